@@ -1,0 +1,8 @@
+#!/bin/sh
+# Build the CPU oracle (test infrastructure). Outputs stay under oracle/_build/ (git-ignored).
+set -e
+cd "$(dirname "$0")"
+mkdir -p _build
+CC=${CC:-gcc}
+$CC -O2 -g -std=c11 -Wall -Wextra -fPIC -shared zflac_oracle.c -o _build/libzflac_oracle.so
+$CC -O3 -march=native -std=c11 -Wall -Wextra -fPIC -shared -DZFO_RELEASE_FAST zflac_oracle.c -o _build/libzflac_oracle_fast.so
