@@ -1,0 +1,128 @@
+/*
+ * zflac_hip.h -- C ABI of the MI355X FLAC decode path (libzflac_hip.so).
+ *
+ * Drop-in boundary for Senryoku/zflac `pub fn decode(allocator, reader) !DecodedFLAC`
+ * (src/zflac.zig:216-217). zflac's only entry point reads a whole stream through a
+ * std reader and returns caller-owned samples; here the caller hands over the stream
+ * bytes and receives the samples in memory it allocated itself (two-phase: open ->
+ * size -> read), so a Zig shim can keep `DecodedFLAC` and its allocator contract
+ * (src/zflac.zig:18-28, :331). See INTEGRATION.md for the shim.
+ *
+ * All decode work (frame sync scan, subframe decode, fixed/LPC rollback, wasted bits,
+ * stereo decorrelation, left-justify, PCM pack-out) runs in HIP kernels on gfx950.
+ * MD5 verification (src/zflac.zig:267-280) runs on the host over the PCM copied back.
+ * There is no CPU decode fallback: without a usable GPU every call returns
+ * ZFLAC_E_DEVICE.
+ *
+ * Thread safety: handles are independent; a handle must not be used by two threads
+ * at once. No global mutable state besides a lazily initialised per-device context.
+ */
+#ifndef ZFLAC_HIP_H
+#define ZFLAC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes, 1:1 with zflac's error set. */
+#define ZFLAC_OK 0
+#define ZFLAC_E_INVALID_SIGNATURE 1         /* src/zflac.zig:220 */
+#define ZFLAC_E_INVALID_METADATA_HEADER 2   /* src/zflac.zig:248 */
+#define ZFLAC_E_MISSING_STREAMINFO 3        /* src/zflac.zig:309 */
+#define ZFLAC_E_UNIMPLEMENTED 4             /* src/zflac.zig:263 */
+#define ZFLAC_E_INVALID_CHECKSUM 5          /* src/zflac.zig:280 */
+#define ZFLAC_E_INVALID_FRAME_HEADER 6      /* src/zflac.zig:352,357,361,372,405 */
+#define ZFLAC_E_INCONSISTENT_PARAMETERS 7   /* src/zflac.zig:386,391 */
+#define ZFLAC_E_INVALID_CODED_NUMBER 8      /* src/zflac.zig:206 */
+#define ZFLAC_E_INVALID_SUBFRAME_HEADER 9   /* src/zflac.zig:431,471,542 */
+#define ZFLAC_E_INVALID_RESIDUAL_CODING 10  /* src/zflac.zig:618 */
+#define ZFLAC_E_END_OF_STREAM 11            /* std.io reader EndOfStream */
+#define ZFLAC_E_OUT_OF_MEMORY 12            /* allocator OutOfMemory */
+#define ZFLAC_E_DEVICE 13                   /* HIP runtime failure / no GPU (no zflac equivalent) */
+#define ZFLAC_E_INVALID_ARGUMENT 14         /* bad handle, index or buffer size */
+#define ZFLAC_E_OUT_OF_DOMAIN 15            /* input on which Debug zflac traps */
+
+/* Arm of zflac's `Samples` union (src/zflac.zig:12-16). */
+#define ZFLAC_S8 0
+#define ZFLAC_S16 1
+#define ZFLAC_S32 2
+
+/* Mirrors the scalar fields of zflac.DecodedFLAC (src/zflac.zig:18-23). */
+typedef struct zflac_info {
+    uint8_t channels;        /* DecodedFLAC.channels */
+    uint8_t bits_per_sample; /* DecodedFLAC.bits_per_sample */
+    uint8_t sample_kind;     /* ZFLAC_S8 / ZFLAC_S16 / ZFLAC_S32 */
+    uint8_t reserved;
+    uint32_t sample_rate;    /* DecodedFLAC.sample_rate (u24 in zflac) */
+    uint64_t n_samples;      /* samples.len: interleaved channel-samples */
+    uint64_t samples_bytes;  /* n_samples * sizeof(SampleType) */
+} zflac_info;
+
+/* One input stream: a complete FLAC byte stream in host memory. */
+typedef struct zflac_stream {
+    const uint8_t *data;
+    size_t len;
+} zflac_stream;
+
+/* Per-kernel device time of the last zflac_hip_batch_run (HIP events on the
+ * library's stream). */
+typedef struct zflac_timings {
+    double scan_ms;     /* frame-sync scan + candidate compaction */
+    double decode_ms;   /* subframe decode kernel (the hot path) */
+    double verify_ms;   /* chain verification */
+    double total_ms;    /* first launch -> last event */
+    uint64_t frames;        /* frames decoded */
+    uint64_t input_bytes;   /* compressed frame bytes of decoded frames */
+    uint64_t output_bytes;  /* PCM bytes written */
+    uint64_t samples;       /* channel-samples written */
+} zflac_timings;
+
+typedef struct zflac_batch zflac_batch;
+
+/* ---- single stream: the decode(allocator, reader) replacement --------------- */
+/* Decode `buf` on `device`. On success *out_batch holds the decoded stream and
+ * *info its shape (allocate info->samples_bytes, 32-byte aligned as zflac does,
+ * then call zflac_hip_read). The returned code is the zflac error of the stream
+ * (MD5 is checked by zflac_hip_read). */
+int zflac_hip_open(const uint8_t *buf, size_t len, int device, zflac_batch **out_batch, zflac_info *info);
+/* Copy the samples into caller memory, verify the STREAMINFO MD5
+ * (ZFLAC_E_INVALID_CHECKSUM on mismatch, as src/zflac.zig:279-280), left-justify is
+ * already applied on the device (src/zflac.zig:287-306). */
+int zflac_hip_read(zflac_batch *b, void *out_samples, size_t out_bytes);
+void zflac_hip_close(zflac_batch *b);
+
+/* ---- batches of independent streams (C5 shard) ------------------------------- */
+/* Parse metadata on the host, upload all compressed bytes to HBM and allocate the
+ * device output. Streams are referenced, not copied, until this call returns. */
+int zflac_hip_batch_create(const zflac_stream *streams, size_t n, int device, int flags, zflac_batch **out);
+/* One device-resident decode of every stream of the batch (inputs already in HBM,
+ * outputs left in HBM). Synchronous. Returns ZFLAC_OK or ZFLAC_E_DEVICE; per-stream
+ * zflac errors are reported by zflac_hip_batch_info. */
+int zflac_hip_batch_run(zflac_batch *b);
+/* Per-stream result of the last run: zflac error code, and shape when OK. */
+int zflac_hip_batch_info(zflac_batch *b, size_t i, zflac_info *info);
+/* Copy stream i's samples to host memory; verify_md5 != 0 checks STREAMINFO MD5. */
+int zflac_hip_batch_read(zflac_batch *b, size_t i, void *out, size_t out_bytes, int verify_md5);
+/* Device pointer of stream i's samples (valid until the next run / destroy). */
+const void *zflac_hip_batch_device_samples(zflac_batch *b, size_t i);
+int zflac_hip_batch_timings(zflac_batch *b, zflac_timings *t);
+size_t zflac_hip_batch_size(zflac_batch *b);
+void zflac_hip_batch_destroy(zflac_batch *b);
+
+/* Flags for zflac_hip_batch_create */
+#define ZFLAC_FLAG_TIMING 1        /* record HIP events around each kernel */
+#define ZFLAC_FLAG_FORCE_SLOW 2    /* skip the parallel fast path (testing the sequential path) */
+
+const char *zflac_hip_error_name(int code);
+/* Number of HIP devices visible; 0 means every decode will fail with ZFLAC_E_DEVICE. */
+int zflac_hip_device_count(void);
+/* Library build tag, e.g. "zflac_hip gfx950 r1". */
+const char *zflac_hip_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -30,6 +30,7 @@ class _Config(ctypes.Structure):
         ("write_total", ctypes.c_int), ("extra_metadata", ctypes.c_int), ("verbatim_every", ctypes.c_int),
         ("silence_every", ctypes.c_int), ("rate_code_mode", ctypes.c_int),
         ("tone_amp", ctypes.c_double), ("noise_lsb", ctypes.c_double), ("stereo_corr", ctypes.c_double),
+        ("fault_frame", ctypes.c_int), ("fault_kind", ctypes.c_int),
         ("n_samples", ctypes.c_uint64), ("seed", ctypes.c_uint64),
     ]
 

@@ -104,6 +104,7 @@ struct Encoder {
     int ibits;  // InterType width 16/32/64
     uint64_t partition_counter = 0;
     uint64_t subframe_counter = 0;
+    int fault = 0;  // active fault kind for the frame being written
 
     explicit Encoder(const flacgen_config& cfg) : c(cfg) {
         int aligned = (cfg.bps + 7) / 8 * 8;
@@ -170,8 +171,10 @@ struct Encoder {
             idx += n;
         }
         const int method = need_rice2 ? 1 : 0;
-        bw.put(method, 2);
+        bw.put(fault == 2 ? 2 : method, 2);
+        if (fault == 5 && po == 0 && bs >= 2 * order + 2 && (bs & 1)) po = 1;  // 2^po does not divide bs
         bw.put(po, 4);
+        if (fault == 5) fault = 0;
         idx = 0;
         for (int p = 0; p < np; p++) {
             const int n = psize - (p == 0 ? order : 0);
@@ -286,7 +289,7 @@ struct Encoder {
 
         auto header = [&](int type) {
             bw.put(0, 1);
-            bw.put(type, 6);
+            bw.put(fault == 1 ? 2 : type, 6);
             if (wasted) {
                 bw.put(1, 1);
                 bw.unary(wasted - 1);
@@ -313,7 +316,7 @@ struct Encoder {
                     if (!predict(u, order, q, shift, r)) continue;
                     header(31 + order);
                     for (int i = 0; i < order; i++) bw.put_signed(u[i], cbps);
-                    bw.put(prec - 1, 4);
+                    bw.put(fault == 3 ? 15 : prec - 1, 4);
                     bw.put(shift, 5);
                     for (int j = 0; j < order; j++) bw.put_signed(q[j], prec);
                     write_residual(bw, r, bs, order);
@@ -433,6 +436,7 @@ void flacgen_default_config(flacgen_config* c) {
     c->stereo_corr = 0.8;
     c->n_samples = 4096 * 8;
     c->seed = 1;
+    c->fault_frame = -1;
 }
 
 int flacgen_generate(const flacgen_config* cfg, flacgen_output* out) {
@@ -463,7 +467,11 @@ int flacgen_generate(const flacgen_config* cfg, flacgen_output* out) {
         blocks.push_back(bs);
         left -= bs;
     }
-    // a final 1-sample block is legal only as the last frame; otherwise merge it
+    if (c.fault_kind == 4 && c.fault_frame >= 0 && (size_t)c.fault_frame < blocks.size() &&
+        (size_t)c.fault_frame + 1 < blocks.size()) {
+        blocks[c.fault_frame] -= 1;
+        blocks.insert(blocks.begin() + c.fault_frame + 1, 1);
+    }
     std::vector<uint8_t> frames;
     std::vector<uint64_t> frame_offs;
     std::vector<int32_t> pcm;
@@ -555,7 +563,11 @@ int flacgen_generate(const flacgen_config* cfg, flacgen_output* out) {
         h.push_back(crc8(h.data(), h.size()));
         BitWriter bw;
         bw.buf = h;
-        for (int ch = 0; ch < C; ch++) enc.write_subframe(bw, sub[ch], ubps[ch], side[ch], bs);
+        for (int ch = 0; ch < C; ch++) {
+            enc.fault = (ch == 0 && (int)f == c.fault_frame && c.fault_kind != 4) ? c.fault_kind : 0;
+            enc.write_subframe(bw, sub[ch], ubps[ch], side[ch], bs);
+            enc.fault = 0;
+        }
         bw.align();
         uint16_t crc = crc16(bw.buf.data(), bw.buf.size());
         bw.put(crc, 16);

@@ -42,6 +42,9 @@ typedef struct flacgen_config {
     double tone_amp;       /* total tone amplitude, fraction of full scale */
     double noise_lsb;      /* rms of the white-noise floor, in significant LSBs */
     double stereo_corr;    /* R = corr * L + noise */
+    int fault_frame;       /* frame index to corrupt, -1 = none */
+    int fault_kind;        /* 1 reserved subframe type, 2 residual method 2, 3 LPC precision code 15,
+                              4 that frame has block size 1, 5 partition order not dividing the block */
     uint64_t n_samples;    /* per channel */
     uint64_t seed;
 } flacgen_config;

@@ -1,0 +1,70 @@
+"""CPU tests of the C-ABI boundary: the library loads, exports every symbol the header
+declares, error codes/names are the zflac set, and without a GPU it fails loudly."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import zflac_amd
+from zflac_amd import _lib, errors
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_functions():
+    text = open(os.path.join(ROOT, "include", "zflac_hip.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(zflac_hip_\w+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    L = _lib.load()
+    funcs = _header_functions()
+    assert len(funcs) >= 14
+    for name in funcs:
+        assert hasattr(L, name), name
+        assert name in _lib.SIGNATURES, f"{name} lacks a ctypes signature"
+
+
+def test_error_names_match_zflac_set():
+    L = _lib.load()
+    import oracle
+
+    for code, name in errors.NAMES.items():
+        assert L.zflac_hip_error_name(code).decode() == name
+        assert oracle.ERROR_NAMES[code] == name
+    assert issubclass(errors.InvalidChecksum, errors.ZflacError)
+    assert errors.error_class(5) is errors.InvalidChecksum
+
+
+def test_version_and_device_count():
+    L = _lib.load()
+    assert b"gfx950" in L.zflac_hip_version()
+    assert zflac_amd.device_count() >= 0
+
+
+def test_no_gpu_fails_loudly():
+    if zflac_amd.device_count() > 0:
+        pytest.skip("a GPU is visible; this checks the no-GPU behaviour")
+    with pytest.raises(errors.DeviceError):
+        zflac_amd.decode(b"fLaC\x80\x00\x00\x22" + bytes(34))
+    h = ctypes.c_void_p()
+    rc = _lib.load().zflac_hip_batch_create(None, 0, 0, 0, ctypes.byref(h))
+    assert rc == 13
+
+
+def test_invalid_arguments():
+    L = _lib.load()
+    assert L.zflac_hip_batch_run(None) == 14
+    assert L.zflac_hip_batch_info(None, 0, None) == 14
+    assert L.zflac_hip_batch_read(None, 0, None, 0, 0) == 14
+    assert L.zflac_hip_batch_size(None) == 0
+    L.zflac_hip_batch_destroy(None)
+    L.zflac_hip_close(None)
+
+
+def test_kernels_compiled_for_gfx950():
+    """The shared library embeds a gfx950 code object (hipcc --offload-arch=gfx950)."""
+    blob = open(_lib.lib_path, "rb").read()
+    assert b"gfx950" in blob

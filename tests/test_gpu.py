@@ -1,0 +1,145 @@
+"""GPU parity tests: the HIP decode path (through the C ABI) against the oracle, the
+reference's golden vectors, the committed fixtures and the writer's ground truth.
+Bar: bit-exact samples and identical zflac error names."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import synth
+import zflac_amd
+from zflac_amd import errors
+
+from . import malformed
+from .util import GOLDEN, PARITY_CONFIGS, expected_samples, load_fixture_manifest, load_kats
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu(data):
+    try:
+        d = zflac_amd.decode(data)
+        return "OK", d
+    except errors.ZflacError as e:
+        return type(e).__name__, None
+
+
+def test_native_library_is_the_path(gpu_ready):
+    assert os.path.exists(zflac_amd.lib_path)
+    assert zflac_amd.device_count() >= 1
+
+
+@pytest.mark.parametrize("kat", load_kats(), ids=lambda k: k["name"])
+def test_kat_basic_zig_gpu(gpu_ready, kat):
+    err, d = _gpu(bytes.fromhex(kat["flac_hex"]))
+    assert err == "OK"
+    assert d.channels == kat["channels"]
+    assert getattr(d.samples, kat["sample_kind"]).tolist() == kat["expected"]
+
+
+def test_golden_fixtures_gpu(gpu_ready):
+    for fx in load_fixture_manifest()["fixtures"]:
+        data = open(os.path.join(GOLDEN, fx["file"]), "rb").read()
+        err, d = _gpu(data)
+        assert err == fx["error"], fx["file"]
+        assert hashlib.sha256(d.samples.values.tobytes()).hexdigest() == fx["samples_sha256"], fx["file"]
+
+
+@pytest.mark.parametrize("name", sorted(PARITY_CONFIGS))
+def test_parity_configs(gpu_ready, name):
+    st = synth.generate(**PARITY_CONFIGS[name])
+    r = oracle.decode(st.flac)
+    assert r.error == "OK"
+    err, d = _gpu(st.flac)
+    assert err == "OK", name
+    np.testing.assert_array_equal(d.samples.values, r.samples)
+    np.testing.assert_array_equal(d.samples.values, expected_samples(st))
+    assert (d.channels, d.sample_rate, d.bits_per_sample) == (r.channels, r.sample_rate, r.bits_per_sample)
+
+
+_CASES = malformed.cases()
+
+
+@pytest.mark.parametrize("case", sorted(_CASES))
+def test_malformed_parity(gpu_ready, case):
+    data, _ = _CASES[case]
+    r = oracle.decode(data)
+    err, d = _gpu(data)
+    assert err == r.error, case
+    if err == "OK":
+        np.testing.assert_array_equal(d.samples.values, r.samples)
+
+
+@pytest.mark.parametrize("name", ["c3_ms16_lpc8", "ch3_16", "variable_blocking", "mono8_lpc3",
+                                  "c4_24bit_lpc32_wasted"])
+def test_sequential_path_parity(gpu_ready, name):
+    """The host-planned sequential chain (used when the parallel chain is not certified)."""
+    st = synth.generate(**PARITY_CONFIGS[name])
+    b = zflac_amd.Batch([st.flac], force_slow=True)
+    b.run()
+    d = b.read(0)
+    b.close()
+    np.testing.assert_array_equal(d.samples.values, expected_samples(st))
+
+
+def test_mixed_batch(gpu_ready):
+    """One batch, several stream classes (container, channel count) and malformed members."""
+    names = sorted(PARITY_CONFIGS)
+    streams = [synth.generate(**dict(PARITY_CONFIGS[n], seed=1000 + i)) for i, n in enumerate(names)]
+    bad = [_CASES[c][0] for c in ("bad_sync_frame2", "wrong_md5", "residual_method_2", "bad_crc8_frame1")]
+    datas = [s.flac for s in streams] + bad
+    b = zflac_amd.Batch(datas)
+    b.run()
+    for i, data in enumerate(datas):
+        r = oracle.decode(data)
+        try:
+            d = b.read(i)
+            err = "OK"
+        except errors.ZflacError as e:
+            err, d = type(e).__name__, None
+        assert err == r.error, i
+        if d is not None:
+            np.testing.assert_array_equal(d.samples.values, r.samples)
+    b.close()
+
+
+def test_batch_rerun_is_stable(gpu_ready):
+    streams = [synth.generate(**synth.config_c5(i, n_frames=8)).flac for i in range(40)]
+    b = zflac_amd.Batch(streams, timing=True)
+    outs = []
+    for _ in range(3):
+        b.run()
+        outs.append([b.read(i).samples.values.copy() for i in range(len(streams))])
+    for i in range(len(streams)):
+        np.testing.assert_array_equal(outs[0][i], outs[1][i])
+        np.testing.assert_array_equal(outs[0][i], outs[2][i])
+    t = b.timings()
+    assert t is not None and t.decode_ms > 0
+    b.close()
+
+
+def test_c5_shard_md5_property(gpu_ready):
+    """Full-shape C5 members (32 frames each) at a reduced stream count: every stream's
+    decoded PCM must hash to its STREAMINFO MD5 (checked inside read) and a sample of
+    them must equal the oracle."""
+    cfgs = [synth.config_c5(i) for i in range(96)]
+    streams = synth.generate_many(cfgs)
+    b = zflac_amd.Batch([s.flac for s in streams])
+    b.run()
+    for i, s in enumerate(streams):
+        d = b.read(i, verify_md5=True)
+        if i % 16 == 0:
+            np.testing.assert_array_equal(d.samples.values, oracle.decode(s.flac, "fast").samples)
+    b.close()
+
+
+@pytest.mark.parametrize("cfg", [synth.config_c2(1024), synth.config_c3(1024), synth.config_c4(256)],
+                         ids=["c2", "c3", "c4"])
+def test_large_single_stream(gpu_ready, cfg):
+    """Long single streams: frame-sync scan over ~MBs, MD5 of the whole output."""
+    st = synth.generate(**cfg)
+    err, d = _gpu(st.flac)  # decode() verifies the STREAMINFO MD5
+    assert err == "OK"
+    np.testing.assert_array_equal(d.samples.values, expected_samples(st))

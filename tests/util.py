@@ -1,0 +1,93 @@
+"""Shared helpers for the test suite: expected outputs and malformed-stream builders."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def justified(pcm: np.ndarray, bps: int) -> np.ndarray:
+    """zflac's output convention: left-justify after MD5 (src/zflac.zig:287-306)."""
+    p = pcm.astype(np.int64)
+    if 9 <= bps <= 15:
+        p = p << (16 - bps)
+    elif 17 <= bps <= 31:
+        p = p << (32 - bps)
+    return p
+
+
+def container_dtype(bps: int):
+    a = (bps + 7) // 8 * 8
+    return {8: np.int8, 16: np.int16, 24: np.int32, 32: np.int32}[a]
+
+
+def expected_samples(stream) -> np.ndarray:
+    bps = stream.config["bps"]
+    return justified(stream.pcm, bps).astype(container_dtype(bps))
+
+
+def load_kats():
+    with open(os.path.join(GOLDEN, "basic_kat.json")) as f:
+        return json.load(f)["kats"]
+
+
+def load_fixture_manifest():
+    with open(os.path.join(GOLDEN, "fixtures.json")) as f:
+        return json.load(f)
+
+
+def patch(data: bytes, offset: int, value: int) -> bytes:
+    b = bytearray(data)
+    b[offset] = value
+    return bytes(b)
+
+
+def streaminfo_offset(data: bytes) -> int:
+    """Byte offset of the STREAMINFO body (the generator always writes it first)."""
+    assert data[:4] == b"fLaC" and (data[4] & 0x7F) == 0
+    return 8
+
+
+# Configurations exercised by parity tests (name -> flacgen overrides). Small sizes:
+# the checked oracle decodes each in well under a second.
+PARITY_CONFIGS = {
+    "c2_mono16_fixed2_k4": dict(channels=1, bps=16, block_size=4096, predictor=2, order=2, partition_order=0,
+                                rice_k=4, tone_amp=0.05, noise_lsb=4.5, n_samples=4096 * 6 + 100),
+    "c3_ms16_lpc8": dict(channels=2, bps=16, block_size=4096, predictor=3, order=8, precision=12, max_shift=12,
+                         stereo_mode=10, partition_order=4, n_samples=4096 * 6),
+    "c4_24bit_lpc32_wasted": dict(channels=2, bps=24, block_size=4096, predictor=3, order=32, precision=15,
+                                  max_shift=15, stereo_mode=1, partition_order=4, wasted_bits=4, noise_lsb=256.0,
+                                  escape_every=97, n_samples=4096 * 4),
+    "ls16_fixed_mix": dict(channels=2, bps=16, stereo_mode=8, predictor=2, order=3, block_size=1152,
+                           n_samples=1152 * 7 + 5, verbatim_every=5),
+    "rs16_lpc5": dict(channels=2, bps=16, stereo_mode=9, order=5, block_size=2304, n_samples=2304 * 5),
+    "auto_stereo_lpc12": dict(channels=2, bps=16, stereo_mode=-1, order=12, precision=14, block_size=4608,
+                              n_samples=4608 * 3 + 17, partition_order=3),
+    "mono8_lpc3": dict(channels=1, bps=8, order=3, precision=7, block_size=576, n_samples=576 * 9 + 3),
+    "stereo12_ms": dict(channels=2, bps=12, stereo_mode=10, order=4, block_size=1024, n_samples=1024 * 6),
+    "ms20_lpc16_escape": dict(channels=2, bps=20, stereo_mode=10, order=16, precision=14, block_size=4096,
+                              n_samples=4096 * 3, escape_every=7),
+    "mono24_rice2": dict(channels=1, bps=24, order=8, block_size=4096, n_samples=4096 * 3, rice2=1),
+    "ch3_16": dict(channels=3, bps=16, order=6, block_size=2048, n_samples=2048 * 4 + 1),
+    "ch6_24_wasted": dict(channels=6, bps=24, order=10, precision=14, block_size=1024, n_samples=1024 * 3,
+                          wasted_bits=2),
+    "ch8_16_fixed": dict(channels=8, bps=16, predictor=2, order=2, block_size=512, n_samples=512 * 5),
+    "stereo32": dict(channels=2, bps=32, stereo_mode=1, order=8, precision=15, block_size=4096,
+                     n_samples=4096 * 2, tone_amp=0.2, noise_lsb=1e6),
+    "variable_blocking": dict(channels=2, bps=16, variable_blocking=1, block_size=3000, n_samples=20000),
+    "unknown_total": dict(channels=2, bps=16, write_total=0, block_size=4096, n_samples=4096 * 3 + 7),
+    "silence_constant": dict(channels=2, bps=16, stereo_mode=1, silence_every=2, block_size=4096,
+                             n_samples=4096 * 4),
+    "extra_metadata": dict(channels=2, bps=16, extra_metadata=1, n_samples=4096 * 2, rate_code_mode=1,
+                           sample_rate=37800),
+    "blocksize16": dict(channels=1, bps=16, predictor=2, order=2, block_size=16, n_samples=16 * 300 + 1),
+    "rate_div10": dict(channels=2, bps=16, rate_code_mode=2, sample_rate=44100, n_samples=4096 * 2),
+    "rate_streaminfo": dict(channels=2, bps=16, rate_code_mode=3, sample_rate=96000, n_samples=4096 * 2),
+    "verbatim_all": dict(channels=2, bps=16, predictor=0, stereo_mode=1, block_size=1024, n_samples=1024 * 4),
+    "odd_block_4095": dict(channels=2, bps=16, block_size=4095, partition_order=0, n_samples=4095 * 3),
+    "lpc32_16bit": dict(channels=2, bps=16, stereo_mode=10, order=32, precision=12, block_size=4096,
+                        n_samples=4096 * 2),
+}

@@ -1,0 +1,47 @@
+"""Build libzflac_hip.so in-tree (hipcc, gfx950). Used by __graft_entry__.build()."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libzflac_hip.so")
+SOURCES = [os.path.join(CSRC, "kernels.hip"), os.path.join(CSRC, "host.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "md5.hpp"),
+                  os.path.join(ROOT, "include", "zflac_hip.h")]
+ARCH = os.environ.get("ZFLAC_OFFLOAD_ARCH", "gfx950")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(d) > t for d in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return LIB
+    objs = []
+    build_dir = os.path.join(HERE, "_build")
+    os.makedirs(build_dir, exist_ok=True)
+    for src in SOURCES:
+        obj = os.path.join(build_dir, os.path.basename(src) + ".o")
+        cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-Wall",
+               "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+        if src.endswith(".hip"):
+            cmd[1:1] = ["-x", "hip"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+        objs.append(obj)
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+    subprocess.check_call(cmd)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

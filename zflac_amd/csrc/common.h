@@ -1,0 +1,133 @@
+// common.h -- descriptors shared by the host planner (host.cpp) and the HIP kernels
+// (kernels.hip). Plain structs, identical layout on both sides.
+#pragma once
+#include <cstdint>
+
+namespace zflac {
+
+enum Err : int {
+    E_OK = 0,
+    E_INVALID_SIGNATURE = 1,
+    E_INVALID_METADATA_HEADER = 2,
+    E_MISSING_STREAMINFO = 3,
+    E_UNIMPLEMENTED = 4,
+    E_INVALID_CHECKSUM = 5,
+    E_INVALID_FRAME_HEADER = 6,
+    E_INCONSISTENT_PARAMETERS = 7,
+    E_INVALID_CODED_NUMBER = 8,
+    E_INVALID_SUBFRAME_HEADER = 9,
+    E_INVALID_RESIDUAL_CODING = 10,
+    E_END_OF_STREAM = 11,
+    E_OUT_OF_MEMORY = 12,
+    E_DEVICE = 13,
+    E_INVALID_ARGUMENT = 14,
+    E_OUT_OF_DOMAIN = 15,
+};
+
+// One stream of a batch, as the kernels see it. Byte offsets are absolute in the
+// batch's input buffer; sample offsets are absolute element indices in the batch's
+// output buffer (one SampleType per element).
+struct StreamDesc {
+    uint64_t in_begin;     // first frame header (right after the metadata blocks)
+    uint64_t in_end;       // end of the stream bytes
+    uint64_t out_base;     // first output element of this stream
+    uint64_t out_cap;      // output elements reserved for this stream
+    uint64_t total;        // STREAMINFO total samples * channels (0 when unknown)
+    uint32_t rate_hz;      // sample rate of the first frame (consistency filter)
+    uint32_t si_rate;      // STREAMINFO sample rate (frame rate code 0)
+    uint32_t first_chunk;  // chunk range of this stream in the sync-scan chunk table
+    uint32_t end_chunk;    // one past the last chunk
+    uint8_t byte1;         // 0xF8 / 0xF9 of the first frame (blocking strategy)
+    uint8_t nch;           // channel count of the first frame (== STREAMINFO)
+    uint8_t dcode;         // bit-depth code of the first frame
+    uint8_t si_bps;        // STREAMINFO bits per sample
+    uint8_t valid_total;   // STREAMINFO total samples > 0
+    uint8_t justify;       // left-justify shift applied at pack-out (src/zflac.zig:287-306)
+    uint8_t pad_[2];
+};
+
+struct ChunkDesc {
+    uint64_t begin;   // absolute byte range scanned for frame-sync candidates
+    uint64_t end;
+    uint32_t stream;
+    uint32_t pad_;
+};
+
+// c_info packing for a decoded candidate frame
+//   bits  0..15  block size - 1
+//   bits 16..19  channel assignment code
+//   bits 20..22  bit-depth code
+//   bit  28      the frame error arose in the header before the consistency checks
+//   bit  29      the header's CRC-8 byte is missing (EndOfStream after the checks)
+constexpr uint32_t INFO_PRE_ERR = 1u << 28;
+constexpr uint32_t INFO_CRC_EOF = 1u << 29;
+
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_BYTES_PER_THREAD = 128;
+constexpr uint64_t CHUNK_BYTES = (uint64_t)SCAN_THREADS * SCAN_BYTES_PER_THREAD;  // 32 KiB
+constexpr int CHUNK_CAP = 64;           // candidates kept per chunk by the scan pass
+constexpr uint64_t INPUT_PAD = 4096;    // zero bytes after the last stream
+
+struct ScanArgs {
+    const uint8_t* in;
+    const StreamDesc* streams;
+    const ChunkDesc* chunks;
+    uint32_t n_chunks;
+    uint32_t* chunk_cnt;        // candidates per chunk (exact)
+    unsigned long long* chunk_units;  // sum of block_size*channels per chunk
+    uint64_t* chunk_slots;      // CHUNK_CAP positions per chunk
+    uint32_t* chunk_slot_units; // CHUNK_CAP units per chunk
+};
+
+struct CompactArgs {
+    const uint8_t* in;
+    const StreamDesc* streams;
+    const ChunkDesc* chunks;
+    uint32_t n_chunks;
+    const uint32_t* chunk_cnt;
+    const uint64_t* chunk_slots;
+    const uint32_t* chunk_slot_units;
+    const uint32_t* chunk_off;             // exclusive scan of chunk_cnt (n_chunks + 1)
+    const unsigned long long* chunk_uoff;  // exclusive scan of chunk_units (n_chunks + 1)
+    uint32_t cap;                          // candidate table capacity
+    uint64_t* c_pos;
+    uint32_t* c_stream;
+    uint64_t* c_out;
+    uint32_t* overflow;                    // set when the table is too small
+};
+
+struct DecodeArgs {
+    const uint8_t* in;
+    void* out;
+    const StreamDesc* streams;
+    const uint64_t* c_pos;
+    const uint32_t* c_stream;
+    const uint64_t* c_out;
+    const uint32_t* n_frames;  // device count (fast path) ...
+    uint32_t n_frames_host;    // ... or host count when n_frames == nullptr
+    uint32_t cap;
+    uint64_t* c_end;
+    int32_t* c_err;
+    uint32_t* c_info;
+    uint32_t* c_rate;
+    int nch;
+    int write;
+};
+
+struct VerifyArgs {
+    const StreamDesc* streams;
+    uint32_t n_streams;
+    const uint32_t* chunk_off;  // per-chunk candidate offsets (n_chunks + 1)
+    const uint64_t* c_pos;
+    const uint32_t* c_stream;
+    const uint64_t* c_out;
+    const uint32_t* n_frames;
+    uint32_t cap;
+    const uint64_t* c_end;
+    const int32_t* c_err;
+    const uint32_t* c_info;
+    const uint32_t* c_rate;
+    uint32_t* status;           // per stream: nonzero => take the sequential path
+};
+
+}  // namespace zflac

@@ -1,0 +1,921 @@
+// host.cpp -- host side of libzflac_hip.so: metadata parsing, batch planning, device
+// buffers and launches, the sequential chain planner for streams the parallel fast path
+// cannot certify, MD5 verification, and the extern "C" ABI of include/zflac_hip.h.
+//
+// Reference: Senryoku/zflac src/zflac.zig (decode :217-310, decode_frames :312-602).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/zflac_hip.h"
+#include "common.h"
+#include "md5.hpp"
+
+namespace zflac {
+
+hipError_t launch_scan(const ScanArgs& a, hipStream_t st);
+hipError_t launch_scan_chunks(const uint32_t* cnt, const unsigned long long* units, uint32_t n, uint32_t* off,
+                              unsigned long long* uoff, uint32_t* n_frames, hipStream_t st);
+hipError_t launch_compact(const CompactArgs& a, hipStream_t st);
+hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
+hipError_t launch_verify(const VerifyArgs& a, uint32_t max_items, hipStream_t st);
+
+namespace {
+
+struct DeviceError {};
+inline void ck(hipError_t e) {
+    if (e != hipSuccess) throw DeviceError{};
+}
+
+// ---------------------------------------------------------------------------------
+// Host-side parsing with zflac semantics
+// ---------------------------------------------------------------------------------
+struct ByteReader {
+    const uint8_t* d;
+    size_t n;
+    size_t pos = 0;
+    bool get(size_t k, uint64_t& v) {  // readInt(uK*8, .big)
+        if (n - pos < k) return false;
+        v = 0;
+        for (size_t i = 0; i < k; i++) v = (v << 8) | d[pos + i];
+        pos += k;
+        return true;
+    }
+};
+
+struct StreamInfoH {
+    uint16_t min_block = 0, max_block = 0;
+    uint32_t sample_rate = 0;
+    uint32_t channels = 0;  // count
+    uint32_t bps = 0;       // bits
+    uint64_t total = 0;     // per channel
+    uint8_t md5[16] = {};
+};
+
+// decode() up to the first frame (src/zflac.zig:217-253)
+int parse_metadata(const uint8_t* d, size_t n, StreamInfoH& si, size_t& frames_begin) {
+    ByteReader r{d, n};
+    uint64_t v;
+    if (!r.get(4, v)) return E_END_OF_STREAM;
+    if (v != 0x664C6143) return E_INVALID_SIGNATURE;  // :218-220
+    bool have = false;
+    for (;;) {
+        uint64_t h;
+        if (!r.get(4, h)) return E_END_OF_STREAM;
+        const unsigned info = (unsigned)(h >> 24) & 0x7F;
+        const bool last = (h >> 31) & 1;
+        const uint64_t length = h & 0xFFFFFF;
+        if (info == 0) {  // STREAMINFO, always 34 bytes (:228-240)
+            if (r.n - r.pos < 34) return E_END_OF_STREAM;
+            const uint8_t* p = d + r.pos;
+            si.min_block = (uint16_t)((p[0] << 8) | p[1]);
+            si.max_block = (uint16_t)((p[2] << 8) | p[3]);
+            si.sample_rate = ((uint32_t)p[10] << 12) | ((uint32_t)p[11] << 4) | (p[12] >> 4);
+            si.channels = ((p[12] >> 1) & 7) + 1;
+            si.bps = (((p[12] & 1) << 4) | (p[13] >> 4)) + 1;
+            si.total = ((uint64_t)(p[13] & 15) << 32) | ((uint64_t)p[14] << 24) | ((uint64_t)p[15] << 16) |
+                       ((uint64_t)p[16] << 8) | p[17];
+            std::memcpy(si.md5, p + 18, 16);
+            r.pos += 34;
+            have = true;
+        } else if (info >= 1 && info <= 6) {  // skipped (:243-247)
+            if (r.n - r.pos < length) return E_END_OF_STREAM;
+            r.pos += length;
+        } else {
+            return E_INVALID_METADATA_HEADER;  // :248
+        }
+        if (last) break;
+    }
+    if (!have) return E_MISSING_STREAMINFO;  // :309
+    frames_begin = r.pos;
+    return E_OK;
+}
+
+int channels_count_h(uint32_t code) { return code <= 7 ? (int)code + 1 : (code <= 10 ? 2 : 0); }
+int depth_bits_h(uint32_t dcode, int si_bps) {
+    static const int B[8] = {0, 8, 12, -1, 16, 20, 24, 32};
+    return dcode == 0 ? si_bps : B[dcode];
+}
+
+struct FrameHdrH {
+    uint32_t bs = 0, rate = 0, chan_code = 0, dcode = 0, byte1 = 0;
+    int err = 0;       // before the consistency checks
+    bool crc_eof = false;
+};
+
+// Frame header (src/zflac.zig:343-375, 203-214, 407), host copy of the device parser.
+FrameHdrH parse_frame_header_h(const uint8_t* p, uint64_t avail, uint32_t si_rate) {
+    FrameHdrH h;
+    if (avail < 4) { h.err = E_END_OF_STREAM; return h; }
+    const uint32_t b0 = p[0], b1 = p[1], b2 = p[2], b3 = p[3];
+    h.byte1 = b1;
+    h.chan_code = b3 >> 4;
+    h.dcode = (b3 >> 1) & 7;
+    if (((b0 << 7) | (b1 >> 1)) != 0x7FFC) { h.err = E_INVALID_FRAME_HEADER; return h; }
+    uint64_t idx = 4;
+    if (avail <= idx) { h.err = E_END_OF_STREAM; return h; }
+    const uint32_t first = p[idx++];
+    uint32_t ones = 0;
+    while (ones < 8 && (first & (0x80u >> ones))) ones++;
+    if (first == 0xFF || ones == 1) { h.err = E_INVALID_CODED_NUMBER; return h; }
+    if (ones >= 2) {
+        if (avail < idx + (ones - 1)) { h.err = E_END_OF_STREAM; return h; }
+        idx += ones - 1;
+    }
+    const uint32_t bc = b2 >> 4;
+    if (bc == 0) { h.err = E_INVALID_FRAME_HEADER; return h; }
+    if (bc == 6) {
+        if (avail <= idx) { h.err = E_END_OF_STREAM; return h; }
+        h.bs = (uint32_t)p[idx++] + 1;
+    } else if (bc == 7) {
+        if (avail < idx + 2) { h.err = E_END_OF_STREAM; return h; }
+        const uint32_t v = ((uint32_t)p[idx] << 8) | p[idx + 1];
+        idx += 2;
+        if (v == 0xFFFF) { h.err = E_INVALID_FRAME_HEADER; return h; }
+        h.bs = v + 1;
+    } else if (bc == 1) {
+        h.bs = 192;
+    } else if (bc <= 5) {
+        h.bs = 144u << bc;
+    } else {
+        h.bs = 1u << bc;
+    }
+    static const uint32_t T[12] = {0, 88200, 176400, 192000, 8000, 16000, 22050, 24000, 32000, 44100, 48000, 96000};
+    const uint32_t rc = b2 & 15;
+    if (rc == 0) {
+        h.rate = si_rate;
+    } else if (rc == 12) {
+        if (avail <= idx) { h.err = E_END_OF_STREAM; return h; }
+        h.rate = p[idx++];
+    } else if (rc == 13 || rc == 14) {
+        if (avail < idx + 2) { h.err = E_END_OF_STREAM; return h; }
+        h.rate = ((uint32_t)p[idx] << 8) | p[idx + 1];
+        if (rc == 14) h.rate *= 10;
+        idx += 2;
+    } else if (rc == 15) {
+        h.err = E_INVALID_FRAME_HEADER;
+        return h;
+    } else {
+        h.rate = T[rc];
+    }
+    if (avail <= idx) h.crc_eof = true;
+    return h;
+}
+
+// ---------------------------------------------------------------------------------
+// Device memory helpers
+// ---------------------------------------------------------------------------------
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void alloc(size_t count) {
+        if (count <= n && p) return;
+        release();
+        ck(hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(count, 1) * sizeof(T)));
+        n = count;
+    }
+};
+
+struct StreamState {
+    // host parse
+    int host_err = 0;  // error known without the GPU (metadata / first frame header)
+    StreamInfoH si;
+    size_t len = 0;
+    size_t frames_begin = 0;
+    int kind = 1;
+    int nch = 0;
+    FrameHdrH first;
+    bool no_frames = false;  // empty frame section, total unknown: zero samples, no error
+    int cls = -1;
+    uint32_t slot = 0;  // index inside its class
+    // result
+    int err = 0;
+    zflac_info info = {};
+    const void* dev_samples = nullptr;  // device pointer of the decoded samples
+    std::unique_ptr<DevBuf<uint8_t>> override_out;
+};
+
+struct Class {
+    int kind = 1;
+    int nch = 2;
+    std::vector<uint32_t> members;  // stream indices
+    std::vector<StreamDesc> desc;
+    std::vector<ChunkDesc> chunks;
+    uint64_t in_bytes = 0, out_elems = 0;
+    uint32_t cap = 0;
+    DevBuf<uint8_t> in;
+    DevBuf<uint8_t> out;
+    DevBuf<StreamDesc> d_desc;
+    DevBuf<ChunkDesc> d_chunks;
+    DevBuf<uint32_t> chunk_cnt, chunk_off, chunk_slot_units, misc, status;
+    DevBuf<unsigned long long> chunk_units, chunk_uoff;
+    DevBuf<uint64_t> chunk_slots;
+    DevBuf<uint64_t> c_pos, c_out, c_end;
+    DevBuf<uint32_t> c_stream, c_info, c_rate;
+    DevBuf<int32_t> c_err;
+    std::vector<uint32_t> h_status;
+    uint32_t h_misc[4] = {0, 0, 0, 0};  // [0] n_frames, [1] overflow
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------
+// Batch
+// ---------------------------------------------------------------------------------
+}  // namespace zflac
+
+struct zflac_batch {
+    int device = 0;
+    int flags = 0;
+    hipStream_t stream = nullptr;
+    std::vector<zflac::StreamState> streams;
+    std::vector<std::unique_ptr<zflac::Class>> classes;
+    hipEvent_t ev[8] = {};
+    bool have_timing = false;
+    zflac_timings timings = {};
+    ~zflac_batch() {
+        classes.clear();
+        for (auto& s : streams) s.override_out.reset();
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace zflac {
+namespace {
+
+int kind_of_bps(uint32_t bps) {
+    const uint32_t aligned = (bps + 7) / 8 * 8;  // src/zflac.zig:256-264
+    if (aligned == 8) return 0;
+    if (aligned == 16) return 1;
+    return 2;
+}
+int esz_of_kind(int kind) { return kind == 0 ? 1 : (kind == 1 ? 2 : 4); }
+uint8_t justify_of(uint32_t bps) {  // src/zflac.zig:287-306
+    if (bps >= 9 && bps <= 15) return (uint8_t)(16 - bps);
+    if (bps >= 17 && bps <= 31) return (uint8_t)(32 - bps);
+    return 0;
+}
+
+// Host planning of one stream: metadata and the first frame header.
+void plan_stream(StreamState& s, const uint8_t* d, size_t n) {
+    s.len = n;
+    s.host_err = parse_metadata(d, n, s.si, s.frames_begin);
+    if (s.host_err) return;
+    s.kind = kind_of_bps(s.si.bps);
+    s.nch = (int)s.si.channels;
+    const bool valid_total = s.si.total > 0;
+    const uint64_t avail = n - s.frames_begin;
+    if (avail < 4) {  // readInt(u32) of the first frame header fails (:343-350)
+        if (valid_total) s.host_err = E_END_OF_STREAM;
+        else s.no_frames = true;
+        return;
+    }
+    s.first = parse_frame_header_h(d + s.frames_begin, avail, s.si.sample_rate);
+    if (s.first.err) { s.host_err = s.first.err; return; }
+    if (depth_bits_h(s.first.dcode, (int)s.si.bps) < 0) { s.host_err = E_OUT_OF_DOMAIN; return; }  // :143
+    if (channels_count_h(s.first.chan_code) != s.nch) { s.host_err = E_INCONSISTENT_PARAMETERS; return; }  // :386
+}
+
+void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
+    const int esz = esz_of_kind(C.kind);
+    // input layout: each stream 16-byte aligned
+    std::vector<uint64_t> in_off(C.members.size());
+    uint64_t off = 0;
+    for (size_t m = 0; m < C.members.size(); m++) {
+        in_off[m] = off;
+        off += (b->streams[C.members[m]].len + 15) & ~(uint64_t)15;
+    }
+    C.in_bytes = off;
+    C.in.alloc(off + INPUT_PAD);
+    std::vector<uint8_t> staging(off + INPUT_PAD, 0);
+    uint64_t out = 0;
+    uint64_t est_frames = 0;
+    C.desc.resize(C.members.size());
+    C.chunks.clear();
+    for (size_t m = 0; m < C.members.size(); m++) {
+        StreamState& s = b->streams[C.members[m]];
+        s.slot = (uint32_t)m;
+        std::memcpy(staging.data() + in_off[m], src[C.members[m]].data, s.len);
+        StreamDesc& D = C.desc[m];
+        std::memset(&D, 0, sizeof(D));
+        D.in_begin = in_off[m] + s.frames_begin;
+        D.in_end = in_off[m] + s.len;
+        D.out_base = out;
+        D.valid_total = s.si.total > 0;
+        D.total = D.valid_total ? s.si.total * (uint64_t)s.nch : 0;
+        D.out_cap = D.total;
+        out += D.out_cap;
+        D.rate_hz = s.first.rate;
+        D.si_rate = s.si.sample_rate;
+        D.byte1 = (uint8_t)s.first.byte1;
+        D.nch = (uint8_t)s.nch;
+        D.dcode = (uint8_t)s.first.dcode;
+        D.si_bps = (uint8_t)s.si.bps;
+        D.justify = justify_of(s.si.bps);
+        D.first_chunk = (uint32_t)C.chunks.size();
+        const uint64_t abase0 = D.in_begin & ~(uint64_t)15;
+        for (uint64_t a = abase0; a < D.in_end; a += CHUNK_BYTES) {
+            ChunkDesc ch;
+            ch.begin = std::max(a, D.in_begin);
+            ch.end = std::min(a + CHUNK_BYTES, D.in_end);
+            ch.stream = (uint32_t)m;
+            ch.pad_ = 0;
+            C.chunks.push_back(ch);
+        }
+        D.end_chunk = (uint32_t)C.chunks.size();
+        const uint64_t minb = std::max<uint64_t>(16, s.si.min_block ? s.si.min_block : 16);
+        est_frames += (s.si.total ? s.si.total / minb : (s.len / 16)) + 2;
+    }
+    C.out_elems = out;
+    C.out.alloc(out * esz + 16);
+    ck(hipMemcpy(C.in.p, staging.data(), staging.size(), hipMemcpyHostToDevice));
+    C.d_desc.alloc(C.desc.size());
+    ck(hipMemcpy(C.d_desc.p, C.desc.data(), C.desc.size() * sizeof(StreamDesc), hipMemcpyHostToDevice));
+    const size_t nc = std::max<size_t>(C.chunks.size(), 1);
+    C.d_chunks.alloc(nc);
+    if (!C.chunks.empty())
+        ck(hipMemcpy(C.d_chunks.p, C.chunks.data(), C.chunks.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice));
+    C.chunk_cnt.alloc(nc);
+    C.chunk_units.alloc(nc);
+    C.chunk_slots.alloc(nc * CHUNK_CAP);
+    C.chunk_slot_units.alloc(nc * CHUNK_CAP);
+    C.chunk_off.alloc(nc + 1);
+    C.chunk_uoff.alloc(nc + 1);
+    C.misc.alloc(4);
+    C.status.alloc(C.members.size());
+    C.h_status.assign(C.members.size(), 0);
+    C.cap = (uint32_t)std::min<uint64_t>(est_frames + C.chunks.size() * 2 + 1024, 0x7FFFFFFFull);
+}
+
+void alloc_candidates(Class& C) {
+    C.c_pos.alloc(C.cap);
+    C.c_out.alloc(C.cap);
+    C.c_end.alloc(C.cap);
+    C.c_stream.alloc(C.cap);
+    C.c_info.alloc(C.cap);
+    C.c_rate.alloc(C.cap);
+    C.c_err.alloc(C.cap);
+}
+
+DecodeArgs decode_args(Class& C) {
+    DecodeArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.in = C.in.p;
+    a.out = C.out.p;
+    a.streams = C.d_desc.p;
+    a.c_pos = C.c_pos.p;
+    a.c_stream = C.c_stream.p;
+    a.c_out = C.c_out.p;
+    a.n_frames = C.misc.p;
+    a.cap = C.cap;
+    a.c_end = C.c_end.p;
+    a.c_err = C.c_err.p;
+    a.c_info = C.c_info.p;
+    a.c_rate = C.c_rate.p;
+    a.nch = C.nch;
+    a.write = 1;
+    return a;
+}
+
+// Launch the whole parallel pipeline of one class on the batch stream.
+void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last) {
+    hipStream_t st = b->stream;
+    const uint32_t nch = (uint32_t)C.chunks.size();
+    ck(hipMemsetAsync(C.status.p, 0, C.members.size() * sizeof(uint32_t), st));
+    ck(hipMemsetAsync(C.misc.p, 0, 4 * sizeof(uint32_t), st));
+    if (timing_first) ck(hipEventRecord(b->ev[0], st));
+    ScanArgs sa;
+    sa.in = C.in.p;
+    sa.streams = C.d_desc.p;
+    sa.chunks = C.d_chunks.p;
+    sa.n_chunks = nch;
+    sa.chunk_cnt = C.chunk_cnt.p;
+    sa.chunk_units = C.chunk_units.p;
+    sa.chunk_slots = C.chunk_slots.p;
+    sa.chunk_slot_units = C.chunk_slot_units.p;
+    ck(launch_scan(sa, st));
+    if (nch) ck(launch_scan_chunks(C.chunk_cnt.p, C.chunk_units.p, nch, C.chunk_off.p, C.chunk_uoff.p, C.misc.p, st));
+    CompactArgs ca;
+    ca.in = C.in.p;
+    ca.streams = C.d_desc.p;
+    ca.chunks = C.d_chunks.p;
+    ca.n_chunks = nch;
+    ca.chunk_cnt = C.chunk_cnt.p;
+    ca.chunk_slots = C.chunk_slots.p;
+    ca.chunk_slot_units = C.chunk_slot_units.p;
+    ca.chunk_off = C.chunk_off.p;
+    ca.chunk_uoff = C.chunk_uoff.p;
+    ca.cap = C.cap;
+    ca.c_pos = C.c_pos.p;
+    ca.c_stream = C.c_stream.p;
+    ca.c_out = C.c_out.p;
+    ca.overflow = C.misc.p + 1;
+    ck(launch_compact(ca, st));
+    if (timing_last) ck(hipEventRecord(b->ev[1], st));
+    DecodeArgs da = decode_args(C);
+    ck(launch_decode(C.kind, da, C.cap, st));
+    if (timing_last) ck(hipEventRecord(b->ev[2], st));
+    VerifyArgs va;
+    va.streams = C.d_desc.p;
+    va.n_streams = (uint32_t)C.members.size();
+    va.chunk_off = C.chunk_off.p;
+    va.c_pos = C.c_pos.p;
+    va.c_stream = C.c_stream.p;
+    va.c_out = C.c_out.p;
+    va.n_frames = C.misc.p;
+    va.cap = C.cap;
+    va.c_end = C.c_end.p;
+    va.c_err = C.c_err.p;
+    va.c_info = C.c_info.p;
+    va.c_rate = C.c_rate.p;
+    va.status = C.status.p;
+    ck(launch_verify(va, C.cap, st));
+    if (timing_last) ck(hipEventRecord(b->ev[3], st));
+    ck(hipMemcpyAsync(C.h_status.data(), C.status.p, C.members.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    ck(hipMemcpyAsync(C.h_misc, C.misc.p, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+}
+
+// ---------------------------------------------------------------------------------
+// Sequential chain planner (src/zflac.zig:340-581 state machine) for streams the
+// fast path could not certify. Frame records come from the fast pass when the chain
+// position is a sync candidate, otherwise from a one-frame device probe.
+// ---------------------------------------------------------------------------------
+struct FrameRec {
+    uint64_t end;
+    int32_t err;
+    uint32_t info;
+    uint32_t rate;
+};
+
+struct SeqRunner {
+    zflac_batch* b;
+    Class& C;
+    uint32_t slot;
+    DevBuf<uint64_t> p_pos, p_out, p_end;
+    DevBuf<uint32_t> p_stream, p_info, p_rate;
+    DevBuf<int32_t> p_err;
+    DevBuf<StreamDesc> p_desc;
+
+    SeqRunner(zflac_batch* b_, Class& C_, uint32_t slot_) : b(b_), C(C_), slot(slot_) {}
+
+    // decode the explicit frame list `pos` (absolute input offsets) with output offsets
+    // `outoff` relative to `desc.out_base`; returns records
+    void run_list(const std::vector<uint64_t>& pos, const std::vector<uint64_t>& outoff, const StreamDesc& desc,
+                  void* out, int write, std::vector<FrameRec>& recs) {
+        const size_t n = pos.size();
+        p_pos.alloc(n);
+        p_out.alloc(n);
+        p_end.alloc(n);
+        p_stream.alloc(n);
+        p_info.alloc(n);
+        p_rate.alloc(n);
+        p_err.alloc(n);
+        p_desc.alloc(1);
+        std::vector<uint32_t> zeros(n, 0);
+        hipStream_t st = b->stream;
+        ck(hipMemcpyAsync(p_pos.p, pos.data(), n * 8, hipMemcpyHostToDevice, st));
+        ck(hipMemcpyAsync(p_out.p, outoff.data(), n * 8, hipMemcpyHostToDevice, st));
+        ck(hipMemcpyAsync(p_stream.p, zeros.data(), n * 4, hipMemcpyHostToDevice, st));
+        ck(hipMemcpyAsync(p_desc.p, &desc, sizeof(desc), hipMemcpyHostToDevice, st));
+        DecodeArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.in = C.in.p;
+        a.out = out;
+        a.streams = p_desc.p;
+        a.c_pos = p_pos.p;
+        a.c_stream = p_stream.p;
+        a.c_out = p_out.p;
+        a.n_frames = nullptr;
+        a.n_frames_host = (uint32_t)n;
+        a.cap = (uint32_t)n;
+        a.c_end = p_end.p;
+        a.c_err = p_err.p;
+        a.c_info = p_info.p;
+        a.c_rate = p_rate.p;
+        a.nch = C.nch;
+        a.write = write;
+        ck(launch_decode(C.kind, a, (uint32_t)n, st));
+        std::vector<uint64_t> e(n);
+        std::vector<int32_t> er(n);
+        std::vector<uint32_t> in(n), ra(n);
+        ck(hipMemcpyAsync(e.data(), p_end.p, n * 8, hipMemcpyDeviceToHost, st));
+        ck(hipMemcpyAsync(er.data(), p_err.p, n * 4, hipMemcpyDeviceToHost, st));
+        ck(hipMemcpyAsync(in.data(), p_info.p, n * 4, hipMemcpyDeviceToHost, st));
+        ck(hipMemcpyAsync(ra.data(), p_rate.p, n * 4, hipMemcpyDeviceToHost, st));
+        ck(hipStreamSynchronize(st));
+        recs.resize(n);
+        for (size_t i = 0; i < n; i++) recs[i] = FrameRec{e[i], er[i], in[i], ra[i]};
+    }
+};
+
+void finish_stream_sequential(zflac_batch* b, Class& C, uint32_t slot, const std::vector<uint32_t>& h_chunk_off,
+                              uint32_t nframes) {
+    StreamState& s = b->streams[C.members[slot]];
+    const StreamDesc D = C.desc[slot];
+    hipStream_t st = b->stream;
+    // fast-pass records of this stream's candidates
+    std::unordered_map<uint64_t, FrameRec> recs;
+    const uint32_t f0 = std::min(h_chunk_off[D.first_chunk], nframes);
+    const uint32_t f1 = std::min(h_chunk_off[D.end_chunk], nframes);
+    if (f1 > f0 && !(b->flags & ZFLAC_FLAG_FORCE_SLOW)) {
+        const size_t n = f1 - f0;
+        std::vector<uint64_t> pos(n), end(n);
+        std::vector<int32_t> err(n);
+        std::vector<uint32_t> info(n), rate(n);
+        ck(hipMemcpyAsync(pos.data(), C.c_pos.p + f0, n * 8, hipMemcpyDeviceToHost, st));
+        ck(hipMemcpyAsync(end.data(), C.c_end.p + f0, n * 8, hipMemcpyDeviceToHost, st));
+        ck(hipMemcpyAsync(err.data(), C.c_err.p + f0, n * 4, hipMemcpyDeviceToHost, st));
+        ck(hipMemcpyAsync(info.data(), C.c_info.p + f0, n * 4, hipMemcpyDeviceToHost, st));
+        ck(hipMemcpyAsync(rate.data(), C.c_rate.p + f0, n * 4, hipMemcpyDeviceToHost, st));
+        ck(hipStreamSynchronize(st));
+        for (size_t i = 0; i < n; i++) recs[pos[i]] = FrameRec{end[i], err[i], info[i], rate[i]};
+    }
+    SeqRunner R(b, C, slot);
+    StreamDesc probe_desc = D;
+    probe_desc.out_base = 0;
+    probe_desc.out_cap = 0;
+    probe_desc.valid_total = 0;
+    probe_desc.total = 0;
+
+    // state machine of decode_frames (src/zflac.zig:321-581)
+    bool valid_total = s.si.total > 0;
+    const uint64_t expC = s.si.channels;
+    const uint64_t total = expC * (valid_total ? s.si.total : 4096);
+    uint64_t buf_len = total;
+    uint64_t offset = 0;
+    uint64_t p = D.in_begin;
+    bool first = true;
+    uint32_t rate0 = 0, count0 = 0, dcode0 = 0;
+    int bps0 = 0;
+    std::vector<uint64_t> list_pos, list_out;
+    int err = 0;
+    for (;;) {
+        if (valid_total && offset >= total) break;  // :341
+        if (D.in_end - p < 4) {                     // :343-350
+            if (valid_total) err = E_END_OF_STREAM;
+            break;
+        }
+        FrameRec rec;
+        auto it = recs.find(p);
+        if (it != recs.end()) {
+            rec = it->second;
+        } else {
+            std::vector<FrameRec> one;
+            R.run_list({p}, {0}, probe_desc, C.out.p, 0, one);
+            rec = one[0];
+        }
+        if (rec.info & INFO_PRE_ERR) { err = rec.err; break; }
+        const uint32_t bs = (rec.info & 0xFFFF) + 1, code = (rec.info >> 16) & 15, dcode = (rec.info >> 20) & 7;
+        if (first) {  // :376-388
+            rate0 = rec.rate;
+            count0 = (uint32_t)channels_count_h(code);
+            dcode0 = dcode;
+            bps0 = depth_bits_h(dcode, (int)s.si.bps);
+            if (bps0 < 0) { err = E_OUT_OF_DOMAIN; break; }
+            if (count0 != expC) { err = E_INCONSISTENT_PARAMETERS; break; }
+            first = false;
+        } else if (rate0 != rec.rate || count0 != (uint32_t)channels_count_h(code) || dcode0 != dcode) {
+            err = E_INCONSISTENT_PARAMETERS;  // :391
+            break;
+        }
+        const uint64_t expected = offset + (uint64_t)bs * count0;  // :394-402
+        if (buf_len < expected) {
+            buf_len = std::max(2 * buf_len, expected);
+            valid_total = false;
+        }
+        if (bs == 1 && valid_total && offset + count0 < total) { err = E_INVALID_FRAME_HEADER; break; }  // :405
+        if (rec.info & INFO_CRC_EOF) { err = E_END_OF_STREAM; break; }
+        if (rec.err) { err = rec.err; break; }
+        list_pos.push_back(p);
+        list_out.push_back(offset);
+        offset += (uint64_t)bs * count0;
+        p = rec.end;
+    }
+    s.err = err;
+    if (err) return;
+    // final decode of the certified chain into this stream's region (or an override)
+    const int esz = esz_of_kind(C.kind);
+    StreamDesc wd = D;
+    wd.out_base = 0;
+    wd.out_cap = offset;
+    wd.valid_total = 0;
+    wd.total = 0;
+    uint8_t* dst;
+    if (offset <= D.out_cap) {
+        dst = C.out.p + D.out_base * esz;
+    } else {
+        s.override_out.reset(new DevBuf<uint8_t>());
+        s.override_out->alloc(offset * esz + 16);
+        dst = s.override_out->p;
+    }
+    if (!list_pos.empty()) {
+        std::vector<FrameRec> out_recs;
+        R.run_list(list_pos, list_out, wd, dst, 1, out_recs);
+        for (auto& r : out_recs)
+            if (r.err) { s.err = r.err; return; }
+    }
+    s.dev_samples = dst;
+    s.info.n_samples = offset;
+    s.info.channels = (uint8_t)count0;
+    s.info.sample_rate = rate0;
+    s.info.bits_per_sample = (uint8_t)bps0;
+}
+
+void run_batch(zflac_batch* b) {
+    ck(hipSetDevice(b->device));
+    const bool timing = (b->flags & ZFLAC_FLAG_TIMING) != 0;
+    for (size_t ci = 0; ci < b->classes.size(); ci++) {
+        Class& C = *b->classes[ci];
+        for (int attempt = 0; attempt < 3; attempt++) {
+            alloc_candidates(C);
+            enqueue_class(b, C, timing && ci == 0, timing && ci + 1 == b->classes.size());
+            ck(hipStreamSynchronize(b->stream));
+            if (!C.h_misc[1] && C.h_misc[0] <= C.cap) break;
+            C.cap = std::max<uint32_t>(C.h_misc[0] + 1024, C.cap * 2);  // candidate table overflow: grow, redo
+        }
+    }
+    if (timing && !b->classes.empty()) {
+        float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
+        ck(hipEventElapsedTime(&t01, b->ev[0], b->ev[1]));
+        ck(hipEventElapsedTime(&t12, b->ev[1], b->ev[2]));
+        ck(hipEventElapsedTime(&t23, b->ev[2], b->ev[3]));
+        ck(hipEventElapsedTime(&t03, b->ev[0], b->ev[3]));
+        b->timings.scan_ms = t01;
+        b->timings.decode_ms = t12;
+        b->timings.verify_ms = t23;
+        b->timings.total_ms = t03;
+        b->have_timing = true;
+    }
+    // results
+    uint64_t frames = 0, in_bytes = 0, out_bytes = 0, samples = 0;
+    for (auto& cp : b->classes) {
+        Class& C = *cp;
+        const int esz = esz_of_kind(C.kind);
+        std::vector<uint32_t> h_off;
+        for (size_t m = 0; m < C.members.size(); m++) {
+            StreamState& s = b->streams[C.members[m]];
+            s.override_out.reset();
+            s.info = zflac_info{};
+            s.info.sample_kind = (uint8_t)C.kind;
+            if (C.h_status[m] == 0 && !(b->flags & ZFLAC_FLAG_FORCE_SLOW)) {
+                const StreamDesc& D = C.desc[m];
+                s.err = 0;
+                s.dev_samples = C.out.p + D.out_base * esz;
+                s.info.n_samples = D.total;
+                s.info.channels = (uint8_t)s.nch;
+                s.info.sample_rate = s.first.rate;
+                s.info.bits_per_sample = (uint8_t)depth_bits_h(s.first.dcode, (int)s.si.bps);
+            } else {
+                if (h_off.empty()) {
+                    h_off.resize(C.chunks.size() + 1);
+                    ck(hipMemcpy(h_off.data(), C.chunk_off.p, h_off.size() * 4, hipMemcpyDeviceToHost));
+                }
+                finish_stream_sequential(b, C, (uint32_t)m, h_off, std::min(C.h_misc[0], C.cap));
+            }
+            s.info.samples_bytes = s.info.n_samples * esz;
+            if (!s.err) {
+                in_bytes += s.len - s.frames_begin;
+                out_bytes += s.info.samples_bytes;
+                samples += s.info.n_samples;
+            }
+        }
+        frames += std::min(C.h_misc[0], C.cap);
+    }
+    b->timings.frames = frames;
+    b->timings.input_bytes = in_bytes;
+    b->timings.output_bytes = out_bytes;
+    b->timings.samples = samples;
+}
+
+// MD5 of the decoded stream exactly as zflac hashes it: before left-justify, 24-bit
+// containers hash 3 bytes per sample (src/zflac.zig:267-280).
+bool md5_matches(const StreamState& s, const void* host_samples) {
+    Md5 md;
+    const uint64_t n = s.info.n_samples;
+    const uint32_t bps = s.si.bps;
+    const uint8_t js = justify_of(bps);
+    if (s.kind == 0) {
+        md.update(host_samples, n);
+    } else if (s.kind == 1) {
+        if (!js) {
+            md.update(host_samples, n * 2);
+        } else {
+            const int16_t* v = static_cast<const int16_t*>(host_samples);
+            std::vector<int16_t> tmp(4096);
+            for (uint64_t i = 0; i < n; i += tmp.size()) {
+                const uint64_t m = std::min<uint64_t>(tmp.size(), n - i);
+                for (uint64_t k = 0; k < m; k++) tmp[k] = (int16_t)(v[i + k] >> js);
+                md.update(tmp.data(), m * 2);
+            }
+        }
+    } else {
+        const int32_t* v = static_cast<const int32_t*>(host_samples);
+        const uint32_t aligned = (bps + 7) / 8 * 8;
+        if (aligned == 32 && !js) {
+            md.update(host_samples, n * 4);
+        } else {
+            const int w = aligned == 24 ? 3 : 4;
+            std::vector<uint8_t> tmp(4096 * 4);
+            for (uint64_t i = 0; i < n; i += 4096) {
+                const uint64_t m = std::min<uint64_t>(4096, n - i);
+                for (uint64_t k = 0; k < m; k++) {
+                    const uint32_t x = (uint32_t)(v[i + k] >> js);
+                    for (int bb = 0; bb < w; bb++) tmp[k * w + bb] = (uint8_t)(x >> (8 * bb));
+                }
+                md.update(tmp.data(), m * w);
+            }
+        }
+    }
+    uint8_t dig[16];
+    md.finish(dig);
+    return std::memcmp(dig, s.si.md5, 16) == 0;
+}
+
+int create_batch(const zflac_stream* streams, size_t n, int device, int flags, zflac_batch** out) {
+    if (!out || (n && !streams)) return E_INVALID_ARGUMENT;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) return E_DEVICE;
+    std::unique_ptr<zflac_batch> b(new (std::nothrow) zflac_batch());
+    if (!b) return E_OUT_OF_MEMORY;
+    b->device = device;
+    b->flags = flags;
+    try {
+        ck(hipSetDevice(device));
+        ck(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+        for (auto& e : b->ev) ck(hipEventCreate(&e));
+        b->streams.resize(n);
+        for (size_t i = 0; i < n; i++) {
+            if (!streams[i].data && streams[i].len) return E_INVALID_ARGUMENT;
+            plan_stream(b->streams[i], streams[i].data, streams[i].len);
+        }
+        for (size_t i = 0; i < n; i++) {
+            StreamState& s = b->streams[i];
+            if (s.host_err || s.no_frames) continue;
+            int ci = -1;
+            for (size_t k = 0; k < b->classes.size(); k++)
+                if (b->classes[k]->kind == s.kind && b->classes[k]->nch == s.nch) ci = (int)k;
+            if (ci < 0) {
+                b->classes.emplace_back(new Class());
+                b->classes.back()->kind = s.kind;
+                b->classes.back()->nch = s.nch;
+                ci = (int)b->classes.size() - 1;
+            }
+            s.cls = ci;
+            b->classes[ci]->members.push_back((uint32_t)i);
+        }
+        for (auto& C : b->classes) alloc_class(b.get(), *C, streams);
+        // streams resolved on the host
+        for (auto& s : b->streams) {
+            if (s.host_err) s.err = s.host_err;
+            if (s.no_frames) {
+                s.err = 0;
+                s.info = zflac_info{};
+                s.info.sample_kind = (uint8_t)s.kind;
+            }
+        }
+    } catch (const DeviceError&) {
+        return E_DEVICE;
+    } catch (const std::bad_alloc&) {
+        return E_OUT_OF_MEMORY;
+    }
+    *out = b.release();
+    return E_OK;
+}
+
+}  // namespace
+}  // namespace zflac
+
+// ---------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------
+using namespace zflac;
+
+extern "C" {
+
+const char* zflac_hip_error_name(int code) {
+    switch (code) {
+        case 0: return "OK";
+        case 1: return "InvalidSignature";
+        case 2: return "InvalidMetadataHeader";
+        case 3: return "MissingStreaminfo";
+        case 4: return "Unimplemented";
+        case 5: return "InvalidChecksum";
+        case 6: return "InvalidFrameHeader";
+        case 7: return "InconsistentParameters";
+        case 8: return "InvalidCodedNumber";
+        case 9: return "InvalidSubframeHeader";
+        case 10: return "InvalidResidualCodingMethod";
+        case 11: return "EndOfStream";
+        case 12: return "OutOfMemory";
+        case 13: return "DeviceError";
+        case 14: return "InvalidArgument";
+        case 15: return "OutOfDomain";
+        default: return "Unknown";
+    }
+}
+
+int zflac_hip_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* zflac_hip_version(void) { return "zflac_hip gfx950 r1"; }
+
+int zflac_hip_batch_create(const zflac_stream* streams, size_t n, int device, int flags, zflac_batch** out) {
+    return create_batch(streams, n, device, flags, out);
+}
+
+int zflac_hip_batch_run(zflac_batch* b) {
+    if (!b) return E_INVALID_ARGUMENT;
+    try {
+        run_batch(b);
+    } catch (const DeviceError&) {
+        return E_DEVICE;
+    } catch (const std::bad_alloc&) {
+        return E_OUT_OF_MEMORY;
+    }
+    return E_OK;
+}
+
+size_t zflac_hip_batch_size(zflac_batch* b) { return b ? b->streams.size() : 0; }
+
+int zflac_hip_batch_info(zflac_batch* b, size_t i, zflac_info* info) {
+    if (!b || i >= b->streams.size()) return E_INVALID_ARGUMENT;
+    const StreamState& s = b->streams[i];
+    if (info) *info = s.info;
+    return s.err;
+}
+
+const void* zflac_hip_batch_device_samples(zflac_batch* b, size_t i) {
+    if (!b || i >= b->streams.size() || b->streams[i].err) return nullptr;
+    return b->streams[i].dev_samples;
+}
+
+int zflac_hip_batch_read(zflac_batch* b, size_t i, void* out, size_t out_bytes, int verify_md5) {
+    if (!b || i >= b->streams.size()) return E_INVALID_ARGUMENT;
+    StreamState& s = b->streams[i];
+    if (s.err) return s.err;
+    if (out_bytes < s.info.samples_bytes || (!out && s.info.samples_bytes)) return E_INVALID_ARGUMENT;
+    try {
+        ck(hipSetDevice(b->device));
+        if (s.info.samples_bytes)
+            ck(hipMemcpy(out, s.dev_samples, s.info.samples_bytes, hipMemcpyDeviceToHost));
+    } catch (const DeviceError&) {
+        return E_DEVICE;
+    }
+    if (verify_md5 && !md5_matches(s, out)) return E_INVALID_CHECKSUM;  // :279-280
+    return E_OK;
+}
+
+int zflac_hip_batch_timings(zflac_batch* b, zflac_timings* t) {
+    if (!b || !t) return E_INVALID_ARGUMENT;
+    *t = b->timings;
+    return b->have_timing ? E_OK : E_INVALID_ARGUMENT;
+}
+
+void zflac_hip_batch_destroy(zflac_batch* b) {
+    if (!b) return;
+    (void)hipSetDevice(b->device);
+    delete b;
+}
+
+int zflac_hip_open(const uint8_t* buf, size_t len, int device, zflac_batch** out_batch, zflac_info* info) {
+    if (!out_batch) return E_INVALID_ARGUMENT;
+    zflac_stream s{buf, len};
+    int rc = create_batch(&s, 1, device, 0, out_batch);
+    if (rc) return rc;
+    rc = zflac_hip_batch_run(*out_batch);
+    if (rc) return rc;
+    return zflac_hip_batch_info(*out_batch, 0, info);
+}
+
+int zflac_hip_read(zflac_batch* b, void* out_samples, size_t out_bytes) {
+    return zflac_hip_batch_read(b, 0, out_samples, out_bytes, 1);
+}
+
+void zflac_hip_close(zflac_batch* b) { zflac_hip_batch_destroy(b); }
+
+}  // extern "C"
