@@ -971,8 +971,11 @@ __device__ inline void decode_subframe(LaneCtx& L, BitReader& br, const FrameCtx
                                L.left >= (uint32_t)L_ && base >= (uint32_t)L.order && (!need_pack || fc.packed);
         const bool need_slow = active && !lane_fast;
         if (__builtin_amdgcn_ballot_w64(need_slow) == 0) {
+            // lanes that are not fast (finished or idle) run the chunk on a scratch reader
+            const BitReader keep = br;
             fast_chunk<KIND, M, L_>(L, br, ring, coef, base, fc, out, nch, c, stereo_pair, lane_fast);
             if (lane_fast) L.left -= L_;
+            else br = keep;
         } else {
             slow_chunk<KIND, M, L_>(L, br, ring, coef, base, fc, out, nch, c, stereo_pair);
         }
