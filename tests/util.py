@@ -77,6 +77,13 @@ PARITY_CONFIGS = {
     "ch8_16_fixed": dict(channels=8, bps=16, predictor=2, order=2, block_size=512, n_samples=512 * 5),
     "stereo32": dict(channels=2, bps=32, stereo_mode=1, order=8, precision=15, block_size=4096,
                      n_samples=4096 * 2, tone_amp=0.2, noise_lsb=1e6),
+    # long Rice codes: forced k with residuals ~2^k+4, so q + 1 + k crosses 32 bits often
+    "longcodes24_k16": dict(channels=2, bps=24, stereo_mode=8, order=4, precision=14, block_size=4096,
+                            n_samples=4096 * 2, rice_k=16, rice2=1, noise_lsb=float(2 ** 19)),
+    "longcodes32_k26": dict(channels=1, bps=32, order=2, predictor=2, block_size=2048, n_samples=2048 * 3,
+                            rice_k=26, rice2=1, noise_lsb=float(2 ** 29), tone_amp=0.0),
+    "longcodes16_k3": dict(channels=2, bps=16, stereo_mode=10, order=8, precision=12, block_size=4096,
+                           n_samples=4096 * 2, rice_k=3, partition_order=2, noise_lsb=300.0),
     "variable_blocking": dict(channels=2, bps=16, variable_blocking=1, block_size=3000, n_samples=20000),
     "unknown_total": dict(channels=2, bps=16, write_total=0, block_size=4096, n_samples=4096 * 3 + 7),
     "silence_constant": dict(channels=2, bps=16, stereo_mode=1, silence_every=2, block_size=4096,

@@ -9,9 +9,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libzflac_hip.so")
-SOURCES = [os.path.join(CSRC, "kernels.hip"), os.path.join(CSRC, "host.cpp")]
-DEPS = SOURCES + [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "md5.hpp"),
-                  os.path.join(ROOT, "include", "zflac_hip.h")]
+SOURCES = [os.path.join(CSRC, n) for n in ("decode_k1.hip", "decode_k2.hip", "decode_k0.hip", "scan.hip",
+                                          "host.cpp")]
+HEADERS = [os.path.join(CSRC, n) for n in ("common.h", "md5.hpp", "device_common.h", "decode.inc")]
+DEPS = SOURCES + HEADERS + [os.path.join(ROOT, "include", "zflac_hip.h")]
 ARCH = os.environ.get("ZFLAC_OFFLOAD_ARCH", "gfx950")
 
 
@@ -28,7 +29,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objs = []
     build_dir = os.path.join(HERE, "_build")
     os.makedirs(build_dir, exist_ok=True)
-    for src in SOURCES:
+    procs = []
+    for src in SOURCES:  # translation units compile in parallel
         obj = os.path.join(build_dir, os.path.basename(src) + ".o")
         cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-Wall",
                "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
@@ -36,8 +38,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
             cmd[1:1] = ["-x", "hip"]
         if verbose:
             print(" ".join(cmd))
-        subprocess.check_call(cmd)
+        procs.append((src, subprocess.Popen(cmd)))
         objs.append(obj)
+    failed = [src for src, p in procs if p.wait() != 0]
+    if failed:
+        raise RuntimeError(f"hipcc failed for {failed}")
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
     subprocess.check_call(cmd)
     return LIB

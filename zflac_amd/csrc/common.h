@@ -112,6 +112,7 @@ struct DecodeArgs {
     uint32_t* c_rate;
     int nch;
     int write;
+    void* dummy;  // >= 64 lanes x 32 bytes: target of masked-off packed stores
 };
 
 struct VerifyArgs {

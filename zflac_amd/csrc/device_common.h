@@ -1,0 +1,159 @@
+// device_common.h -- device helpers shared by the scan and decode translation units:
+// format tables, the exact frame-header parser (src/zflac.zig:343-407) and small utils.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <utility>
+
+#include "common.h"
+
+namespace zflac {
+
+// ----------------------------------------------------------------------------------
+// small helpers
+// ----------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ int channels_count(uint32_t code) {  // Channels.count, src/zflac.zig:107-122
+    return code <= 7 ? (int)code + 1 : (code <= 10 ? 2 : 0);
+}
+__device__ __forceinline__ uint32_t rate_table(uint32_t code) {  // SampleRate.hz, src/zflac.zig:75-90
+    switch (code) {
+        case 1: return 88200;
+        case 2: return 176400;
+        case 3: return 192000;
+        case 4: return 8000;
+        case 5: return 16000;
+        case 6: return 22050;
+        case 7: return 24000;
+        case 8: return 32000;
+        case 9: return 44100;
+        case 10: return 48000;
+        default: return 96000;
+    }
+}
+__device__ __forceinline__ int depth_bits(uint32_t dcode, int si_bps) {  // BitDepth.bps, src/zflac.zig:135-145
+    switch (dcode) {
+        case 0: return si_bps;
+        case 1: return 8;
+        case 2: return 12;
+        case 4: return 16;
+        case 5: return 20;
+        case 6: return 24;
+        case 7: return 32;
+        default: return -1;  // reserved: `unreachable` in zflac
+    }
+}
+
+struct Crc8Table {
+    uint8_t t[256];
+};
+constexpr Crc8Table make_crc8_table() {  // x^8 + x^2 + x + 1, init 0 (RFC 9639 frame header CRC)
+    Crc8Table r{};
+    for (int i = 0; i < 256; i++) {
+        uint32_t c = (uint32_t)i;
+        for (int k = 0; k < 8; k++) c = (c & 0x80) ? ((c << 1) ^ 0x07) & 0xFF : (c << 1) & 0xFF;
+        r.t[i] = (uint8_t)c;
+    }
+    return r;
+}
+static __constant__ Crc8Table CRC8 = make_crc8_table();
+
+// ----------------------------------------------------------------------------------
+// Frame header, exact zflac semantics (src/zflac.zig:343-375, 203-214, 407).
+// `err` holds errors raised before the first-frame / consistency checks; a missing
+// CRC-8 byte is reported separately because zflac reads it after those checks.
+// ----------------------------------------------------------------------------------
+struct FrameHdr {
+    uint32_t bs, rate, hdr_len;
+    uint32_t chan_code, dcode, byte1, zero_bit, bs_code;
+    int err;
+    bool crc_eof;
+    bool crc_ok;
+};
+
+__device__ __forceinline__ FrameHdr parse_frame_header(const uint8_t* p, uint64_t avail, uint32_t si_rate) {
+    FrameHdr h;
+    h.bs = h.rate = h.hdr_len = 0;
+    h.chan_code = h.dcode = h.byte1 = h.zero_bit = h.bs_code = 0;
+    h.err = 0;
+    h.crc_eof = false;
+    h.crc_ok = false;
+    if (avail < 4) { h.err = E_END_OF_STREAM; return h; }
+    const uint32_t b0 = p[0], b1 = p[1], b2 = p[2], b3 = p[3];
+    h.byte1 = b1;
+    h.chan_code = b3 >> 4;
+    h.dcode = (b3 >> 1) & 7;
+    h.zero_bit = b3 & 1;
+    h.bs_code = b2 >> 4;
+    if (((b0 << 7) | (b1 >> 1)) != 0x7FFC) { h.err = E_INVALID_FRAME_HEADER; return h; }  // :351-352
+    uint32_t idx = 4;
+    // read_coded_number (:203-214)
+    if (avail <= idx) { h.err = E_END_OF_STREAM; return h; }
+    const uint32_t first = p[idx++];
+    const uint32_t ones = __clz((~first & 0xFFu) << 24) > 8 ? 8 : __clz((~first & 0xFFu) << 24);
+    if (first == 0xFF || ones == 1) { h.err = E_INVALID_CODED_NUMBER; return h; }
+    if (ones >= 2) {
+        if (avail < (uint64_t)idx + (ones - 1)) { h.err = E_END_OF_STREAM; return h; }
+        idx += ones - 1;
+    }
+    // block size (:356-365)
+    const uint32_t bc = b2 >> 4;
+    if (bc == 0) { h.err = E_INVALID_FRAME_HEADER; return h; }
+    if (bc == 6) {
+        if (avail <= idx) { h.err = E_END_OF_STREAM; return h; }
+        h.bs = (uint32_t)p[idx++] + 1;
+    } else if (bc == 7) {
+        if (avail < (uint64_t)idx + 2) { h.err = E_END_OF_STREAM; return h; }
+        const uint32_t v = ((uint32_t)p[idx] << 8) | p[idx + 1];
+        idx += 2;
+        if (v == 0xFFFF) { h.err = E_INVALID_FRAME_HEADER; return h; }
+        h.bs = v + 1;
+    } else if (bc == 1) {
+        h.bs = 192;
+    } else if (bc <= 5) {
+        h.bs = 144u << bc;
+    } else {
+        h.bs = 1u << bc;
+    }
+    // sample rate (:367-374); uncommon 8-bit rate is taken in Hz as zflac does (:369)
+    const uint32_t rc = b2 & 15;
+    if (rc == 0) {
+        h.rate = si_rate;
+    } else if (rc == 12) {
+        if (avail <= idx) { h.err = E_END_OF_STREAM; return h; }
+        h.rate = p[idx++];
+    } else if (rc == 13 || rc == 14) {
+        if (avail < (uint64_t)idx + 2) { h.err = E_END_OF_STREAM; return h; }
+        h.rate = ((uint32_t)p[idx] << 8) | p[idx + 1];
+        if (rc == 14) h.rate *= 10;
+        idx += 2;
+    } else if (rc == 15) {
+        h.err = E_INVALID_FRAME_HEADER;
+        return h;
+    } else {
+        h.rate = rate_table(rc);
+    }
+    // CRC-8 byte (:407): read, never checked by zflac; checked here only to filter
+    // sync candidates.
+    h.hdr_len = idx + 1;
+    if (avail <= idx) {
+        h.crc_eof = true;
+        return h;
+    }
+    uint32_t crc = 0;
+    for (uint32_t i = 0; i < idx; i++) crc = CRC8.t[crc ^ p[i]];
+    h.crc_ok = crc == p[idx];
+    return h;
+}
+
+// Filter for sync candidates: a well-formed header consistent with the stream's first
+// frame. Anything it rejects that zflac would still decode breaks the verified chain and
+// sends the stream to the sequential planner, so the filter affects speed only.
+__device__ __forceinline__ bool candidate_ok(const FrameHdr& h, const StreamDesc& S) {
+    return h.err == 0 && !h.crc_eof && h.crc_ok && h.zero_bit == 0 && h.byte1 == S.byte1 &&
+           channels_count(h.chan_code) == S.nch && h.dcode == S.dcode && h.rate == S.rate_hz;
+}
+
+}  // namespace zflac

@@ -26,7 +26,14 @@ hipError_t launch_scan(const ScanArgs& a, hipStream_t st);
 hipError_t launch_scan_chunks(const uint32_t* cnt, const unsigned long long* units, uint32_t n, uint32_t* off,
                               unsigned long long* uoff, uint32_t* n_frames, hipStream_t st);
 hipError_t launch_compact(const CompactArgs& a, hipStream_t st);
-hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
+hipError_t launch_decode_k0(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
+hipError_t launch_decode_k1(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
+hipError_t launch_decode_k2(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
+static hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_frames, hipStream_t st) {
+    if (kind == 0) return launch_decode_k0(a, max_frames, st);
+    if (kind == 1) return launch_decode_k1(a, max_frames, st);
+    return launch_decode_k2(a, max_frames, st);
+}
 hipError_t launch_verify(const VerifyArgs& a, uint32_t max_items, hipStream_t st);
 
 namespace {
@@ -232,6 +239,7 @@ struct Class {
     DevBuf<uint64_t> c_pos, c_out, c_end;
     DevBuf<uint32_t> c_stream, c_info, c_rate;
     DevBuf<int32_t> c_err;
+    DevBuf<uint8_t> dummy;  // sink of masked-off packed stores (64 lanes x 32 B)
     std::vector<uint32_t> h_status;
     uint32_t h_misc[4] = {0, 0, 0, 0};  // [0] n_frames, [1] overflow
 };
@@ -363,6 +371,7 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     C.chunk_off.alloc(nc + 1);
     C.chunk_uoff.alloc(nc + 1);
     C.misc.alloc(4);
+    C.dummy.alloc(4096);
     C.status.alloc(C.members.size());
     C.h_status.assign(C.members.size(), 0);
     C.cap = (uint32_t)std::min<uint64_t>(est_frames + C.chunks.size() * 2 + 1024, 0x7FFFFFFFull);
@@ -395,6 +404,7 @@ DecodeArgs decode_args(Class& C) {
     a.c_rate = C.c_rate.p;
     a.nch = C.nch;
     a.write = 1;
+    a.dummy = C.dummy.p;
     return a;
 }
 
@@ -515,6 +525,7 @@ struct SeqRunner {
         a.c_rate = p_rate.p;
         a.nch = C.nch;
         a.write = write;
+        a.dummy = C.dummy.p;
         ck(launch_decode(C.kind, a, (uint32_t)n, st));
         std::vector<uint64_t> e(n);
         std::vector<int32_t> er(n);

@@ -1,0 +1,299 @@
+// scan.hip -- frame-sync scan, candidate compaction and chain verification kernels.
+//
+//   k_scan          frame-sync scan: every input byte once, 16 B/lane coalesced loads;
+//                   candidates = 0xFF 0xF8|F9 + exact header parse + CRC-8 + the stream's
+//                   first-frame parameters. Up to CHUNK_CAP ordered candidates per 32 KiB chunk.
+//   k_scan_chunks   exclusive scan of per-chunk candidate counts / sample units.
+//   k_compact       ordered candidate table (position, stream, output offset).
+//   k_verify        is the candidate chain exactly what zflac's sequential frame loop
+//                   (src/zflac.zig:340-581) would walk? Streams failing it are finished by
+//                   the host's sequential planner.
+#include "device_common.h"
+
+namespace zflac {
+
+// ----------------------------------------------------------------------------------
+// k_scan: frame-sync candidates per 32 KiB chunk
+// ----------------------------------------------------------------------------------
+__device__ inline uint32_t ff_mask(uint32_t d) { return ((d & 0x7F7F7F7Fu) + 0x01010101u) & d & 0x80808080u; }
+
+// Calls fn(position) for every candidate in the 16-byte window at `ws` that lies in
+// [lo, hi). Windows are 16-byte aligned.
+template <typename Fn>
+__device__ inline void scan_window(const uint8_t* in, uint64_t ws, uint64_t lo, uint64_t hi, Fn&& fn) {
+    const uint4 v = *reinterpret_cast<const uint4*>(in + ws);
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        uint32_t m = ff_mask(d[k]);
+        while (m) {
+            const int bit = __ffs(m) - 1;
+            m &= m - 1;
+            const int b = 4 * k + (bit >> 3);
+            uint32_t nxt;
+            if (b < 15) nxt = (d[(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 0xFF;
+            else nxt = in[ws + 16];
+            const uint64_t p = ws + b;
+            if ((nxt & 0xFE) == 0xF8 && p >= lo && p < hi) fn(p);
+        }
+    }
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
+    const uint32_t chunk = blockIdx.x;
+    if (chunk >= a.n_chunks) return;
+    __shared__ uint32_t s_cnt;
+    __shared__ unsigned long long s_units;
+    __shared__ uint64_t s_pos[CHUNK_CAP];
+    __shared__ uint32_t s_u[CHUNK_CAP];
+    const ChunkDesc ch = a.chunks[chunk];
+    const StreamDesc S = a.streams[ch.stream];
+    if (threadIdx.x == 0) {
+        s_cnt = 0;
+        s_units = 0;
+    }
+    __syncthreads();
+    const uint64_t abase = ch.begin & ~(uint64_t)15;
+    for (int r = 0; r < SCAN_BYTES_PER_THREAD / 16; r++) {
+        const uint64_t ws = abase + ((uint64_t)r * SCAN_THREADS + threadIdx.x) * 16;
+        if (ws >= ch.end) break;
+        scan_window(a.in, ws, ch.begin, ch.end, [&](uint64_t p) {
+            const FrameHdr h = parse_frame_header(a.in + p, S.in_end - p, S.si_rate);
+            if (!candidate_ok(h, S)) return;
+            const uint32_t slot = atomicAdd(&s_cnt, 1u);
+            const uint32_t units = h.bs * S.nch;
+            atomicAdd(&s_units, (unsigned long long)units);
+            if (slot < CHUNK_CAP) {
+                s_pos[slot] = p;
+                s_u[slot] = units;
+            }
+        });
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t n = s_cnt;
+        const uint32_t m = n < CHUNK_CAP ? n : CHUNK_CAP;
+        for (uint32_t i = 1; i < m; i++) {  // insertion sort by position (m is tiny)
+            uint64_t p = s_pos[i];
+            uint32_t u = s_u[i];
+            int j = (int)i - 1;
+            while (j >= 0 && s_pos[j] > p) {
+                s_pos[j + 1] = s_pos[j];
+                s_u[j + 1] = s_u[j];
+                j--;
+            }
+            s_pos[j + 1] = p;
+            s_u[j + 1] = u;
+        }
+        a.chunk_cnt[chunk] = n;
+        a.chunk_units[chunk] = s_units;
+    }
+    __syncthreads();
+    const uint32_t m = s_cnt < CHUNK_CAP ? s_cnt : CHUNK_CAP;
+    if (threadIdx.x < m) {
+        a.chunk_slots[(uint64_t)chunk * CHUNK_CAP + threadIdx.x] = s_pos[threadIdx.x];
+        a.chunk_slot_units[(uint64_t)chunk * CHUNK_CAP + threadIdx.x] = s_u[threadIdx.x];
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// k_scan_chunks: single-workgroup exclusive scans (n_chunks is ~input/32KiB)
+// ----------------------------------------------------------------------------------
+constexpr int SCANK_THREADS = 1024;
+
+__global__ __launch_bounds__(SCANK_THREADS) void k_scan_chunks(const uint32_t* cnt, const unsigned long long* units,
+                                                               uint32_t n, uint32_t* off,
+                                                               unsigned long long* uoff, uint32_t* n_frames) {
+    __shared__ uint32_t s_c[SCANK_THREADS];
+    __shared__ unsigned long long s_u[SCANK_THREADS];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (n + SCANK_THREADS - 1) / SCANK_THREADS;
+    const uint32_t lo = t * per, hi = (lo + per < n) ? lo + per : n;
+    uint32_t sc = 0;
+    unsigned long long su = 0;
+    for (uint32_t i = lo; i < hi; i++) {
+        sc += cnt[i];
+        su += units[i];
+    }
+    s_c[t] = sc;
+    s_u[t] = su;
+    __syncthreads();
+    for (uint32_t d = 1; d < SCANK_THREADS; d <<= 1) {  // Hillis-Steele inclusive
+        uint32_t vc = 0;
+        unsigned long long vu = 0;
+        if (t >= d) {
+            vc = s_c[t - d];
+            vu = s_u[t - d];
+        }
+        __syncthreads();
+        s_c[t] += vc;
+        s_u[t] += vu;
+        __syncthreads();
+    }
+    uint32_t rc = t ? s_c[t - 1] : 0;
+    unsigned long long ru = t ? s_u[t - 1] : 0;
+    for (uint32_t i = lo; i < hi; i++) {
+        off[i] = rc;
+        uoff[i] = ru;
+        rc += cnt[i];
+        ru += units[i];
+    }
+    if (t == SCANK_THREADS - 1) {
+        off[n] = s_c[t];
+        uoff[n] = s_u[t];
+        *n_frames = s_c[t];
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// k_compact: ordered candidate table
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(SCAN_THREADS) void k_compact(CompactArgs a) {
+    const uint32_t chunk = blockIdx.x;
+    if (chunk >= a.n_chunks) return;
+    const ChunkDesc ch = a.chunks[chunk];
+    const StreamDesc S = a.streams[ch.stream];
+    const uint32_t n = a.chunk_cnt[chunk];
+    const uint32_t off = a.chunk_off[chunk];
+    const unsigned long long ubase = a.chunk_uoff[S.first_chunk];
+    const unsigned long long u0 = a.chunk_uoff[chunk];
+    if (n <= CHUNK_CAP) {
+        const uint32_t t = threadIdx.x;
+        if (t < n) {
+            unsigned long long pre = 0;
+            for (uint32_t i = 0; i < t; i++) pre += a.chunk_slot_units[(uint64_t)chunk * CHUNK_CAP + i];
+            const uint32_t idx = off + t;
+            if (idx < a.cap) {
+                a.c_pos[idx] = a.chunk_slots[(uint64_t)chunk * CHUNK_CAP + t];
+                a.c_stream[idx] = ch.stream;
+                a.c_out[idx] = S.out_base + (u0 - ubase + pre);
+            } else {
+                atomicOr(a.overflow, 1u);
+            }
+        }
+        return;
+    }
+    // Overflowed chunk (more than CHUNK_CAP candidates): ordered two-pass rescan of each
+    // 4 KiB sub-range with a block-wide exclusive scan.
+    __shared__ uint32_t s_c[SCAN_THREADS];
+    __shared__ unsigned long long s_u[SCAN_THREADS];
+    __shared__ uint32_t s_base_c;
+    __shared__ unsigned long long s_base_u;
+    if (threadIdx.x == 0) {
+        s_base_c = 0;
+        s_base_u = 0;
+    }
+    __syncthreads();
+    const uint64_t abase = ch.begin & ~(uint64_t)15;
+    for (int r = 0; r < SCAN_BYTES_PER_THREAD / 16; r++) {
+        const uint64_t ws = abase + ((uint64_t)r * SCAN_THREADS + threadIdx.x) * 16;
+        uint32_t c = 0;
+        unsigned long long u = 0;
+        if (ws < ch.end) {
+            scan_window(a.in, ws, ch.begin, ch.end, [&](uint64_t p) {
+                const FrameHdr h = parse_frame_header(a.in + p, S.in_end - p, S.si_rate);
+                if (!candidate_ok(h, S)) return;
+                c++;
+                u += h.bs * S.nch;
+            });
+        }
+        s_c[threadIdx.x] = c;
+        s_u[threadIdx.x] = u;
+        __syncthreads();
+        for (uint32_t d = 1; d < SCAN_THREADS; d <<= 1) {
+            uint32_t vc = 0;
+            unsigned long long vu = 0;
+            if (threadIdx.x >= d) {
+                vc = s_c[threadIdx.x - d];
+                vu = s_u[threadIdx.x - d];
+            }
+            __syncthreads();
+            s_c[threadIdx.x] += vc;
+            s_u[threadIdx.x] += vu;
+            __syncthreads();
+        }
+        uint32_t rc = s_base_c + s_c[threadIdx.x] - c;
+        unsigned long long ru = s_base_u + s_u[threadIdx.x] - u;
+        if (ws < ch.end && c) {
+            scan_window(a.in, ws, ch.begin, ch.end, [&](uint64_t p) {
+                const FrameHdr h = parse_frame_header(a.in + p, S.in_end - p, S.si_rate);
+                if (!candidate_ok(h, S)) return;
+                const uint32_t idx = off + rc;
+                if (idx < a.cap) {
+                    a.c_pos[idx] = p;
+                    a.c_stream[idx] = ch.stream;
+                    a.c_out[idx] = S.out_base + (u0 - ubase + ru);
+                } else {
+                    atomicOr(a.overflow, 1u);
+                }
+                rc++;
+                ru += h.bs * S.nch;
+            });
+        }
+        __syncthreads();
+        if (threadIdx.x == SCAN_THREADS - 1) {
+            s_base_c += s_c[threadIdx.x];
+            s_base_u += s_u[threadIdx.x];
+        }
+        __syncthreads();
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// k_verify: is the candidate chain what zflac's frame loop would walk? (see header)
+// ----------------------------------------------------------------------------------
+__global__ void k_verify(VerifyArgs a) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t nframes = *a.n_frames;
+    if (nframes > a.cap) nframes = a.cap;
+    if (t < a.n_streams) {
+        const StreamDesc S = a.streams[t];
+        const uint32_t f0 = a.chunk_off[S.first_chunk], f1 = a.chunk_off[S.end_chunk];
+        if (f1 <= f0 || f1 > nframes || !S.valid_total || a.c_pos[f0] != S.in_begin) atomicOr(&a.status[t], 1u);
+    }
+    if (t >= nframes) return;
+    const uint32_t s = a.c_stream[t];
+    const StreamDesc S = a.streams[s];
+    const uint32_t f1 = min(a.chunk_off[S.end_chunk], nframes);
+    const uint64_t rel = a.c_out[t] - S.out_base;
+    if (S.valid_total && rel >= S.total) return;  // past the last sample: never read (:341)
+    bool bad = a.c_err[t] != 0;
+    const uint32_t info = a.c_info[t];
+    const uint32_t bs = (info & 0xFFFF) + 1;
+    const uint32_t code = (info >> 16) & 15, dcode = (info >> 20) & 7;
+    if ((uint32_t)channels_count(code) != S.nch || dcode != S.dcode || a.c_rate[t] != S.rate_hz) bad = true;
+    const uint64_t units = (uint64_t)bs * S.nch;
+    if (bs == 1 && rel + S.nch < S.total) bad = true;  // :405
+    const uint64_t end_rel = rel + units;
+    if (end_rel > S.total || end_rel > S.out_cap) bad = true;     // zflac would grow the buffer
+    if (end_rel < S.total && (t + 1 >= f1 || a.c_pos[t + 1] != a.c_end[t])) bad = true;
+    if (bad) atomicOr(&a.status[s], 1u);
+}
+
+// ----------------------------------------------------------------------------------
+// launchers
+// ----------------------------------------------------------------------------------
+hipError_t launch_scan(const ScanArgs& a, hipStream_t st) {
+    if (a.n_chunks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scan, dim3(a.n_chunks), dim3(SCAN_THREADS), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_scan_chunks(const uint32_t* cnt, const unsigned long long* units, uint32_t n, uint32_t* off,
+                              unsigned long long* uoff, uint32_t* n_frames, hipStream_t st) {
+    hipLaunchKernelGGL(k_scan_chunks, dim3(1), dim3(SCANK_THREADS), 0, st, cnt, units, n, off, uoff, n_frames);
+    return hipGetLastError();
+}
+hipError_t launch_compact(const CompactArgs& a, hipStream_t st) {
+    if (a.n_chunks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_compact, dim3(a.n_chunks), dim3(SCAN_THREADS), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_verify(const VerifyArgs& a, uint32_t max_items, hipStream_t st) {
+    uint32_t n = max_items > a.n_streams ? max_items : a.n_streams;
+    uint32_t blocks = (n + 255) / 256;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(k_verify, dim3(blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace zflac
