@@ -1,6 +1,7 @@
 #!/bin/bash
-# Collect PMC counters for the bench workload in separate rocprofv3 passes (no tracing
-# domains combined with --pmc). Usage: tools/pmc.sh <tag>
+# Collect PMC counters for the bench workload in separate rocprofv3 passes (counters are
+# never combined with tracing domains), plus the FETCH_SIZE/WRITE_SIZE calibration of
+# tools/calib_pmc.hip. Usage: tools/pmc.sh <tag>   (on the GPU box)
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-pmc}
@@ -8,12 +9,14 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-verify"
-timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAVE_CYCLES"
 P2="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES"
 i=0
-for P in "$P1" "$P2" "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+for P in "$P1" "$P2" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o run -- python3 $R/bench.py $ARGS > $OUT/p$i.log 2>&1 || echo "pass $i failed rc=$?" >> $OUT/status.txt
+  timeout -k 10 300 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o run -- python3 $R/bench.py $ARGS > $OUT/p$i.log 2>&1
+done
+for P in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 120 rocprofv3 --pmc $P --output-format csv -d $OUT/calib_$P -o run -- $R/tools/_build/calib_pmc > $OUT/calib_$P.log 2>&1
 done
 echo done >> $OUT/status.txt

@@ -67,6 +67,7 @@ constexpr int SCAN_BYTES_PER_THREAD = 128;
 constexpr uint64_t CHUNK_BYTES = (uint64_t)SCAN_THREADS * SCAN_BYTES_PER_THREAD;  // 32 KiB
 constexpr int CHUNK_CAP = 64;           // candidates kept per chunk by the scan pass
 constexpr uint64_t INPUT_PAD = 4096;    // zero bytes after the last stream
+constexpr uint64_t DUMMY_BYTES = 64 * 64 * 32;  // 64 wave slots x 64 lanes x 2 quads
 
 struct ScanArgs {
     const uint8_t* in;
@@ -112,7 +113,7 @@ struct DecodeArgs {
     uint32_t* c_rate;
     int nch;
     int write;
-    void* dummy;  // >= 64 lanes x 32 bytes: target of masked-off packed stores
+    void* dummy;  // DUMMY_BYTES: target of masked-off / pending-less packed stores
 };
 
 struct VerifyArgs {

@@ -371,7 +371,7 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     C.chunk_off.alloc(nc + 1);
     C.chunk_uoff.alloc(nc + 1);
     C.misc.alloc(4);
-    C.dummy.alloc(4096);
+    C.dummy.alloc(DUMMY_BYTES);
     C.status.alloc(C.members.size());
     C.h_status.assign(C.members.size(), 0);
     C.cap = (uint32_t)std::min<uint64_t>(est_frames + C.chunks.size() * 2 + 1024, 0x7FFFFFFFull);
