@@ -43,10 +43,11 @@ def parse_args():
     return ap.parse_args()
 
 
-def make_shard(rank: int, n_streams: int):
+def make_shard(rank: int, world: int, n_streams: int):
     import synth
+    from zflac_amd.shard import shard_range
 
-    cfgs = [synth.config_c5(rank * n_streams + i, n_frames=FRAMES_PER_STREAM) for i in range(n_streams)]
+    cfgs = [synth.config_c5(g, n_frames=FRAMES_PER_STREAM) for g in shard_range(rank, world, n_streams)]
     out = [None] * n_streams
     workers = min(16, os.cpu_count() or 1)
 
@@ -139,7 +140,7 @@ def main():
     import zflac_amd
 
     t_gen = time.perf_counter()
-    streams = make_shard(rank, args.streams_per_gpu)
+    streams = make_shard(rank, world, args.streams_per_gpu)
     t_gen = time.perf_counter() - t_gen
     batch = zflac_amd.Batch(streams, device=local_rank, timing=True)
 
@@ -169,26 +170,13 @@ def main():
     samples_rank = tm.samples
     in_bytes, out_bytes = tm.input_bytes, tm.output_bytes
 
-    if dist is not None:
-        import torch
-
-        v = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(v, op=dist.ReduceOp.MAX)
-        elapsed = float(v.item())
-        s = torch.tensor([samples_rank, in_bytes, out_bytes], dtype=torch.float64, device="cuda")
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        samples_all, in_all, out_all = (float(x) for x in s.tolist())
-    else:
-        samples_all, in_all, out_all = float(samples_rank), float(in_bytes), float(out_bytes)
-
     errs = [] if args.no_verify else verify(batch, streams)
-    ok = not errs
-    if dist is not None:
-        import torch
+    from zflac_amd.shard import aggregate
 
-        e = torch.tensor([len(errs)], dtype=torch.int64, device="cuda")
-        dist.all_reduce(e)
-        ok = int(e.item()) == 0
+    tot = aggregate(dist, "cuda" if dist is not None else None, elapsed, samples_rank, in_bytes, out_bytes, len(errs))
+    elapsed = tot.elapsed_s
+    samples_all, in_all, out_all = tot.samples, tot.input_bytes, tot.output_bytes
+    ok = tot.errors == 0
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
