@@ -29,6 +29,23 @@ STREAMS_PER_GPU = 1250
 FRAMES_PER_STREAM = 32
 BLOCK = 4096
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak
+# PMC summary of the current k_decode build (tools/pmc.sh + tools/pmc_summary.py; FETCH_SIZE /
+# WRITE_SIZE corrected by the factors tools/calib_pmc.hip measures for this access pattern)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_current.json")
+
+
+def pmc_traffic(kernel: str):
+    """Corrected HBM bytes per launch of `kernel` from the committed PMC summary, or None."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    row = d.get("kernels", {}).get(kernel)
+    if not row or "hbm_traffic_bytes" not in row:
+        return None
+    return {"bytes": int(row["hbm_traffic_bytes"]), "read": int(row["hbm_read_bytes"]),
+            "write": int(row["hbm_write_bytes"]), "source": os.path.relpath(d.get("_source", PMC_SUMMARY), ROOT)}
 
 
 def parse_args():
@@ -91,7 +108,7 @@ def cpu_baseline(streams, seconds: float):
     dt = time.perf_counter() - t0
     total = sum(counts)
     return {"value": total / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/zflac_oracle.c (-O3 -march=native, Debug checks off) decoding C5 shard streams "
+            "sample": f"oracle/zflac_oracle.c (-O3 -march=x86-64-v4, Debug checks off) decoding C5 shard streams "
                       f"round-robin on {threads} threads for {dt:.1f} s ({total / 1e6:.0f} M samples, MD5 incl.)"}
 
 
@@ -188,6 +205,8 @@ def main():
         dec_avg = float(np.mean(dec_ms))
         alg_bytes = in_bytes + out_bytes  # per decode launch (this rank)
         achieved = alg_bytes / (dec_avg * 1e-3) / 1e9
+        pmc = pmc_traffic("zflac::k_decode<1, 2>")
+        traffic = pmc["bytes"] if pmc else None
         line = {
             "metric": "Msamples/s decoded (bit-exact) + achieved HBM GB/s, 4096-blk stereo",
             "value": round(value, 1),
@@ -208,11 +227,12 @@ def main():
             "hbm_gbs_step": round((in_all + out_all) * args.steps / elapsed / 1e9, 1),
             "bit_exact": ok,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "k_decode<1>", "kernel_ms": round(dec_avg, 4),
                          "alg_bytes_per_launch": int(alg_bytes)},
             "stages_ms": {"scan+compact": round(float(np.mean(scan_ms)), 4), "decode": round(dec_avg, 4),
                           "verify": round(float(np.mean(ver_ms)), 4)},
+            "traffic_detail": pmc,
             "cpu_baseline": cpu,
             "gen_seconds": round(t_gen, 2),
         }

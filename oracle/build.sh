@@ -5,4 +5,4 @@ cd "$(dirname "$0")"
 mkdir -p _build
 CC=${CC:-gcc}
 $CC -O2 -g -std=c11 -Wall -Wextra -fPIC -shared zflac_oracle.c -o _build/libzflac_oracle.so
-$CC -O3 -march=native -std=c11 -Wall -Wextra -fPIC -shared -DZFO_RELEASE_FAST zflac_oracle.c -o _build/libzflac_oracle_fast.so
+$CC -O3 -march=x86-64-v4 -std=c11 -Wall -Wextra -fPIC -shared -DZFO_RELEASE_FAST zflac_oracle.c -o _build/libzflac_oracle_fast.so
