@@ -99,6 +99,7 @@ struct CompactArgs {
 
 struct DecodeArgs {
     const uint8_t* in;
+    uint64_t in_size;          // bytes of `in`, INPUT_PAD included
     void* out;
     const StreamDesc* streams;
     const uint64_t* c_pos;

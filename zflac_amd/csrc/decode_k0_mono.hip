@@ -1,0 +1,9 @@
+// decode_k0_mono.hip -- decode kernel for SampleType container kind 0 (i8), mono layout.
+// One translation unit per (container, layout) so the instantiations compile in parallel.
+#include "decode.inc"
+
+namespace zflac {
+hipError_t launch_decode_k0_mono(const DecodeArgs& a, uint32_t max_frames, hipStream_t st) {
+    return launch_decode_layout<0, LAY_MONO>(a, max_frames, st);
+}
+}  // namespace zflac

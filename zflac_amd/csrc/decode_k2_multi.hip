@@ -1,0 +1,9 @@
+// decode_k2_multi.hip -- decode kernel for SampleType container kind 2 (i32), multi layout.
+// One translation unit per (container, layout) so the instantiations compile in parallel.
+#include "decode.inc"
+
+namespace zflac {
+hipError_t launch_decode_k2_multi(const DecodeArgs& a, uint32_t max_frames, hipStream_t st) {
+    return launch_decode_layout<2, LAY_MULTI>(a, max_frames, st);
+}
+}  // namespace zflac

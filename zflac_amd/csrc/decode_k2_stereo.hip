@@ -1,0 +1,9 @@
+// decode_k2_stereo.hip -- decode kernel for SampleType container kind 2 (i32), stereo layout.
+// One translation unit per (container, layout) so the instantiations compile in parallel.
+#include "decode.inc"
+
+namespace zflac {
+hipError_t launch_decode_k2_stereo(const DecodeArgs& a, uint32_t max_frames, hipStream_t st) {
+    return launch_decode_layout<2, LAY_STEREO>(a, max_frames, st);
+}
+}  // namespace zflac

@@ -26,13 +26,29 @@ hipError_t launch_scan(const ScanArgs& a, hipStream_t st);
 hipError_t launch_scan_chunks(const uint32_t* cnt, const unsigned long long* units, uint32_t n, uint32_t* off,
                               unsigned long long* uoff, uint32_t* n_frames, hipStream_t st);
 hipError_t launch_compact(const CompactArgs& a, hipStream_t st);
-hipError_t launch_decode_k0(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
-hipError_t launch_decode_k1(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
-hipError_t launch_decode_k2(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
+#define ZFLAC_DECL_LAUNCH(K)                                                                  \
+    hipError_t launch_decode_k##K##_stereo(const DecodeArgs& a, uint32_t max_frames, hipStream_t st); \
+    hipError_t launch_decode_k##K##_mono(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);   \
+    hipError_t launch_decode_k##K##_multi(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
+ZFLAC_DECL_LAUNCH(0)
+ZFLAC_DECL_LAUNCH(1)
+ZFLAC_DECL_LAUNCH(2)
+#undef ZFLAC_DECL_LAUNCH
 static hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_frames, hipStream_t st) {
-    if (kind == 0) return launch_decode_k0(a, max_frames, st);
-    if (kind == 1) return launch_decode_k1(a, max_frames, st);
-    return launch_decode_k2(a, max_frames, st);
+    const int lay = a.nch == 2 ? 2 : (a.nch == 1 ? 1 : 0);
+    if (kind == 0) {
+        if (lay == 2) return launch_decode_k0_stereo(a, max_frames, st);
+        if (lay == 1) return launch_decode_k0_mono(a, max_frames, st);
+        return launch_decode_k0_multi(a, max_frames, st);
+    }
+    if (kind == 1) {
+        if (lay == 2) return launch_decode_k1_stereo(a, max_frames, st);
+        if (lay == 1) return launch_decode_k1_mono(a, max_frames, st);
+        return launch_decode_k1_multi(a, max_frames, st);
+    }
+    if (lay == 2) return launch_decode_k2_stereo(a, max_frames, st);
+    if (lay == 1) return launch_decode_k2_mono(a, max_frames, st);
+    return launch_decode_k2_multi(a, max_frames, st);
 }
 hipError_t launch_verify(const VerifyArgs& a, uint32_t max_items, hipStream_t st);
 
@@ -391,6 +407,7 @@ DecodeArgs decode_args(Class& C) {
     DecodeArgs a;
     std::memset(&a, 0, sizeof(a));
     a.in = C.in.p;
+    a.in_size = C.in.n;
     a.out = C.out.p;
     a.streams = C.d_desc.p;
     a.c_pos = C.c_pos.p;
@@ -511,6 +528,7 @@ struct SeqRunner {
         DecodeArgs a;
         std::memset(&a, 0, sizeof(a));
         a.in = C.in.p;
+        a.in_size = C.in.n;
         a.out = out;
         a.streams = p_desc.p;
         a.c_pos = p_pos.p;
