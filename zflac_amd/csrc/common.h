@@ -67,6 +67,7 @@ constexpr int SCAN_BYTES_PER_THREAD = 128;
 constexpr uint64_t CHUNK_BYTES = (uint64_t)SCAN_THREADS * SCAN_BYTES_PER_THREAD;  // 32 KiB
 constexpr int CHUNK_CAP = 64;           // candidates kept per chunk by the scan pass
 constexpr uint64_t INPUT_PAD = 4096;    // zero bytes after the last stream
+constexpr int MAX_CH = 8;               // FLAC channel limit; k_walk's per-frame record stride
 constexpr uint64_t DUMMY_BYTES = 64 * 64 * 32;  // 64 wave slots x 64 lanes x 2 quads
 
 struct ScanArgs {
@@ -115,6 +116,7 @@ struct DecodeArgs {
     int nch;
     int write;
     void* dummy;  // DUMMY_BYTES: target of masked-off / pending-less packed stores
+    uint32_t* sub_start;  // [frame][MAX_CH]: bit offset of subframe c >= 1 (k_walk -> k_decode)
 };
 
 struct VerifyArgs {

@@ -6,4 +6,8 @@ namespace zflac {
 hipError_t launch_decode_k2_stereo(const DecodeArgs& a, uint32_t max_frames, hipStream_t st) {
     return launch_decode_layout<2, LAY_STEREO>(a, max_frames, st);
 }
+// k_walk for this container: used by the stereo and the 3..8-channel layouts
+hipError_t launch_walk_k2(const DecodeArgs& a, uint32_t max_frames, hipStream_t st) {
+    return launch_walk_kind<2>(a, max_frames, st);
+}
 }  // namespace zflac

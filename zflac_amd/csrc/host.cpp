@@ -29,13 +29,19 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t st);
 #define ZFLAC_DECL_LAUNCH(K)                                                                  \
     hipError_t launch_decode_k##K##_stereo(const DecodeArgs& a, uint32_t max_frames, hipStream_t st); \
     hipError_t launch_decode_k##K##_mono(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);   \
-    hipError_t launch_decode_k##K##_multi(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
+    hipError_t launch_decode_k##K##_multi(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);   \
+    hipError_t launch_walk_k##K(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
 ZFLAC_DECL_LAUNCH(0)
 ZFLAC_DECL_LAUNCH(1)
 ZFLAC_DECL_LAUNCH(2)
 #undef ZFLAC_DECL_LAUNCH
 static hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_frames, hipStream_t st) {
     const int lay = a.nch == 2 ? 2 : (a.nch == 1 ? 1 : 0);
+    if (a.nch > 1) {  // subframe start offsets first (k_walk), then the decode proper
+        const hipError_t e = kind == 0 ? launch_walk_k0(a, max_frames, st)
+                                       : (kind == 1 ? launch_walk_k1(a, max_frames, st) : launch_walk_k2(a, max_frames, st));
+        if (e != hipSuccess) return e;
+    }
     if (kind == 0) {
         if (lay == 2) return launch_decode_k0_stereo(a, max_frames, st);
         if (lay == 1) return launch_decode_k0_mono(a, max_frames, st);
@@ -253,7 +259,7 @@ struct Class {
     DevBuf<unsigned long long> chunk_units, chunk_uoff;
     DevBuf<uint64_t> chunk_slots;
     DevBuf<uint64_t> c_pos, c_out, c_end;
-    DevBuf<uint32_t> c_stream, c_info, c_rate;
+    DevBuf<uint32_t> c_stream, c_info, c_rate, sub;
     DevBuf<int32_t> c_err;
     DevBuf<uint8_t> dummy;  // sink of masked-off packed stores (64 lanes x 32 B)
     std::vector<uint32_t> h_status;
@@ -401,6 +407,7 @@ void alloc_candidates(Class& C) {
     C.c_info.alloc(C.cap);
     C.c_rate.alloc(C.cap);
     C.c_err.alloc(C.cap);
+    C.sub.alloc((size_t)C.cap * MAX_CH);
 }
 
 DecodeArgs decode_args(Class& C) {
@@ -422,6 +429,7 @@ DecodeArgs decode_args(Class& C) {
     a.nch = C.nch;
     a.write = 1;
     a.dummy = C.dummy.p;
+    a.sub_start = C.sub.p;
     return a;
 }
 
@@ -502,6 +510,7 @@ struct SeqRunner {
     DevBuf<uint64_t> p_pos, p_out, p_end;
     DevBuf<uint32_t> p_stream, p_info, p_rate;
     DevBuf<int32_t> p_err;
+    DevBuf<uint32_t> p_sub;
     DevBuf<StreamDesc> p_desc;
 
     SeqRunner(zflac_batch* b_, Class& C_, uint32_t slot_) : b(b_), C(C_), slot(slot_) {}
@@ -544,6 +553,8 @@ struct SeqRunner {
         a.nch = C.nch;
         a.write = write;
         a.dummy = C.dummy.p;
+        p_sub.alloc(n * MAX_CH);
+        a.sub_start = p_sub.p;
         ck(launch_decode(C.kind, a, (uint32_t)n, st));
         std::vector<uint64_t> e(n);
         std::vector<int32_t> er(n);
