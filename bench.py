@@ -173,12 +173,14 @@ def main():
     barrier_sync()
     t0 = time.perf_counter()
     dec_ms = []
+    walk_ms = []
     scan_ms = []
     ver_ms = []
     for _ in range(args.steps):
         batch.run()
         t = batch.timings()
         dec_ms.append(t.decode_ms)
+        walk_ms.append(t.walk_ms)
         scan_ms.append(t.scan_ms)
         ver_ms.append(t.verify_ms)
     barrier_sync()
@@ -228,9 +230,10 @@ def main():
             "bit_exact": ok,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_decode<1>", "kernel_ms": round(dec_avg, 4),
+                         "kernel": "k_decode<1, 2>", "kernel_ms": round(dec_avg, 4),
                          "alg_bytes_per_launch": int(alg_bytes)},
-            "stages_ms": {"scan+compact": round(float(np.mean(scan_ms)), 4), "decode": round(dec_avg, 4),
+            "stages_ms": {"scan+compact": round(float(np.mean(scan_ms)), 4),
+                          "walk": round(float(np.mean(walk_ms)), 4), "decode": round(dec_avg, 4),
                           "verify": round(float(np.mean(ver_ms)), 4)},
             "traffic_detail": pmc,
             "cpu_baseline": cpu,

@@ -71,13 +71,14 @@ typedef struct zflac_stream {
  * library's stream). */
 typedef struct zflac_timings {
     double scan_ms;     /* frame-sync scan + candidate compaction */
-    double decode_ms;   /* subframe decode kernel (the hot path) */
+    double decode_ms;   /* subframe decode kernel k_decode (the hot path) */
     double verify_ms;   /* chain verification */
     double total_ms;    /* first launch -> last event */
     uint64_t frames;        /* frames decoded */
     uint64_t input_bytes;   /* compressed frame bytes of decoded frames */
     uint64_t output_bytes;  /* PCM bytes written */
     uint64_t samples;       /* channel-samples written */
+    double walk_ms;     /* subframe-start walk k_walk (2+ channels; runs before k_decode) */
 } zflac_timings;
 
 typedef struct zflac_batch zflac_batch;

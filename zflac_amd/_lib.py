@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-lib_path = os.path.join(_HERE, "libzflac_hip.so")
+# ZFLAC_HIP_LIB selects another build of the same library (timing experiments)
+lib_path = os.environ.get("ZFLAC_HIP_LIB") or os.path.join(_HERE, "libzflac_hip.so")
 
 
 class zflac_info(ctypes.Structure):
@@ -26,7 +27,7 @@ class zflac_stream(ctypes.Structure):
 class zflac_timings(ctypes.Structure):
     _fields_ = [("scan_ms", ctypes.c_double), ("decode_ms", ctypes.c_double), ("verify_ms", ctypes.c_double),
                 ("total_ms", ctypes.c_double), ("frames", ctypes.c_uint64), ("input_bytes", ctypes.c_uint64),
-                ("output_bytes", ctypes.c_uint64), ("samples", ctypes.c_uint64)]
+                ("output_bytes", ctypes.c_uint64), ("samples", ctypes.c_uint64), ("walk_ms", ctypes.c_double)]
 
 
 # every symbol include/zflac_hip.h declares, with (restype, argtypes)

@@ -35,11 +35,18 @@ ZFLAC_DECL_LAUNCH(0)
 ZFLAC_DECL_LAUNCH(1)
 ZFLAC_DECL_LAUNCH(2)
 #undef ZFLAC_DECL_LAUNCH
-static hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_frames, hipStream_t st) {
+// k_walk (subframe start offsets, 2+ channels) then k_decode; `mid` (optional) is recorded
+// between the two launches.
+static hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_frames, hipStream_t st,
+                                hipEvent_t mid = nullptr) {
     const int lay = a.nch == 2 ? 2 : (a.nch == 1 ? 1 : 0);
-    if (a.nch > 1) {  // subframe start offsets first (k_walk), then the decode proper
+    if (a.nch > 1) {
         const hipError_t e = kind == 0 ? launch_walk_k0(a, max_frames, st)
                                        : (kind == 1 ? launch_walk_k1(a, max_frames, st) : launch_walk_k2(a, max_frames, st));
+        if (e != hipSuccess) return e;
+    }
+    if (mid) {
+        const hipError_t e = hipEventRecord(mid, st);
         if (e != hipSuccess) return e;
     }
     if (kind == 0) {
@@ -469,7 +476,7 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     ck(launch_compact(ca, st));
     if (timing_last) ck(hipEventRecord(b->ev[1], st));
     DecodeArgs da = decode_args(C);
-    ck(launch_decode(C.kind, da, C.cap, st));
+    ck(launch_decode(C.kind, da, C.cap, st, timing_last ? b->ev[4] : nullptr));
     if (timing_last) ck(hipEventRecord(b->ev[2], st));
     VerifyArgs va;
     va.streams = C.d_desc.p;
@@ -696,13 +703,15 @@ void run_batch(zflac_batch* b) {
         }
     }
     if (timing && !b->classes.empty()) {
-        float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
+        float t01 = 0, t14 = 0, t42 = 0, t23 = 0, t03 = 0;
         ck(hipEventElapsedTime(&t01, b->ev[0], b->ev[1]));
-        ck(hipEventElapsedTime(&t12, b->ev[1], b->ev[2]));
+        ck(hipEventElapsedTime(&t14, b->ev[1], b->ev[4]));
+        ck(hipEventElapsedTime(&t42, b->ev[4], b->ev[2]));
         ck(hipEventElapsedTime(&t23, b->ev[2], b->ev[3]));
         ck(hipEventElapsedTime(&t03, b->ev[0], b->ev[3]));
         b->timings.scan_ms = t01;
-        b->timings.decode_ms = t12;
+        b->timings.walk_ms = t14;
+        b->timings.decode_ms = t42;
         b->timings.verify_ms = t23;
         b->timings.total_ms = t03;
         b->have_timing = true;
