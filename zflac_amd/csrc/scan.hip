@@ -17,11 +17,10 @@ namespace zflac {
 // ----------------------------------------------------------------------------------
 __device__ inline uint32_t ff_mask(uint32_t d) { return ((d & 0x7F7F7F7Fu) + 0x01010101u) & d & 0x80808080u; }
 
-// Calls fn(position) for every candidate in the 16-byte window at `ws` that lies in
+// Calls fn(position) for every candidate in the 16-byte window `v` at `ws` that lies in
 // [lo, hi). Windows are 16-byte aligned.
 template <typename Fn>
-__device__ inline void scan_window(const uint8_t* in, uint64_t ws, uint64_t lo, uint64_t hi, Fn&& fn) {
-    const uint4 v = *reinterpret_cast<const uint4*>(in + ws);
+__device__ inline void scan_window_v(const uint4 v, const uint8_t* in, uint64_t ws, uint64_t lo, uint64_t hi, Fn&& fn) {
     const uint32_t d[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -37,6 +36,10 @@ __device__ inline void scan_window(const uint8_t* in, uint64_t ws, uint64_t lo, 
             if ((nxt & 0xFE) == 0xF8 && p >= lo && p < hi) fn(p);
         }
     }
+}
+template <typename Fn>
+__device__ inline void scan_window(const uint8_t* in, uint64_t ws, uint64_t lo, uint64_t hi, Fn&& fn) {
+    scan_window_v(*reinterpret_cast<const uint4*>(in + ws), in, ws, lo, hi, fn);
 }
 
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
@@ -54,10 +57,19 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     }
     __syncthreads();
     const uint64_t abase = ch.begin & ~(uint64_t)15;
-    for (int r = 0; r < SCAN_BYTES_PER_THREAD / 16; r++) {
+    // all of the thread's windows in flight at once (coalesced 4 KiB rows per round)
+    constexpr int R = SCAN_BYTES_PER_THREAD / 16;
+    uint4 v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint64_t ws = abase + ((uint64_t)r * SCAN_THREADS + threadIdx.x) * 16;
+        v[r] = ws < ch.end ? *reinterpret_cast<const uint4*>(a.in + ws) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
         const uint64_t ws = abase + ((uint64_t)r * SCAN_THREADS + threadIdx.x) * 16;
         if (ws >= ch.end) break;
-        scan_window(a.in, ws, ch.begin, ch.end, [&](uint64_t p) {
+        scan_window_v(v[r], a.in, ws, ch.begin, ch.end, [&](uint64_t p) {
             const FrameHdr h = parse_frame_header(a.in + p, S.in_end - p, S.si_rate);
             if (!candidate_ok(h, S)) return;
             const uint32_t slot = atomicAdd(&s_cnt, 1u);
