@@ -1,0 +1,34 @@
+"""Timing-probe run (experimental build with -DZFLAC_PROBE, exp/libzflac_hip_probe.so):
+cycles per chunk phase of k_walk and k_decode, summed over waves, for the C5 shard.
+Usage: ZFLAC_HIP_LIB=exp/libzflac_hip_probe.so python tools/probe.py [streams]"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import synth  # noqa: E402
+import zflac_amd  # noqa: E402
+from zflac_amd import _lib  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1250
+streams = [s.flac for s in synth.generate_many([synth.config_c5(i) for i in range(n)])]
+b = zflac_amd.Batch(streams, timing=True)
+L = _lib.load()
+fn = L.zflac_hip_probe
+fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+buf = (ctypes.c_ulonglong * 16)()
+b.run()
+fn(b._h, buf, 16)  # discard the warm-up run
+b.run()
+fn(b._h, buf, 16)
+t = b.timings()
+names = ["topup", "fast", "slow", "chunks", "fast_chunks", "redos"]
+out = {"streams": n, "walk_ms": t.walk_ms, "decode_ms": t.decode_ms}
+for k, base in (("walk", 0), ("decode", 8)):
+    v = [buf[base + i] for i in range(6)]
+    ch = max(1, v[3])
+    out[k] = {names[i]: v[i] for i in range(6)}
+    out[k]["cycles_per_chunk"] = {names[i]: round(v[i] / ch, 1) for i in range(3)}
+print(json.dumps(out, indent=1))

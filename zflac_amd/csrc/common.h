@@ -69,6 +69,7 @@ constexpr int CHUNK_CAP = 64;           // candidates kept per chunk by the scan
 constexpr uint64_t INPUT_PAD = 4096;    // zero bytes after the last stream
 constexpr int MAX_CH = 8;               // FLAC channel limit; k_walk's per-frame record stride
 constexpr uint64_t DUMMY_BYTES = 64 * 64 * 32;  // 64 wave slots x 64 lanes x 2 quads
+constexpr uint64_t PROBE_BYTES = 256;           // after the dummy region: timing-probe builds only
 
 struct ScanArgs {
     const uint8_t* in;

@@ -400,7 +400,7 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     C.chunk_off.alloc(nc + 1);
     C.chunk_uoff.alloc(nc + 1);
     C.misc.alloc(4);
-    C.dummy.alloc(DUMMY_BYTES);
+    C.dummy.alloc(DUMMY_BYTES + PROBE_BYTES);
     C.status.alloc(C.members.size());
     C.h_status.assign(C.members.size(), 0);
     C.cap = (uint32_t)std::min<uint64_t>(est_frames + C.chunks.size() * 2 + 1024, 0x7FFFFFFFull);
@@ -944,6 +944,19 @@ int zflac_hip_batch_timings(zflac_batch* b, zflac_timings* t) {
     *t = b->timings;
     return b->have_timing ? E_OK : E_INVALID_ARGUMENT;
 }
+
+#ifdef ZFLAC_PROBE
+// Timing-probe build only (tools/probe.sh): cycle counters the decode kernels accumulate
+// behind the dummy store region of the first class; zeroed after reading.
+extern "C" int zflac_hip_probe(zflac_batch* b, unsigned long long* out, int n) {
+    if (!b || b->classes.empty() || n > (int)(PROBE_BYTES / 8)) return E_INVALID_ARGUMENT;
+    auto& C = *b->classes[0];
+    uint8_t* p = reinterpret_cast<uint8_t*>(C.dummy.p) + DUMMY_BYTES;
+    if (hipMemcpy(out, p, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return E_DEVICE;
+    if (hipMemset(p, 0, PROBE_BYTES) != hipSuccess) return E_DEVICE;
+    return E_OK;
+}
+#endif
 
 void zflac_hip_batch_destroy(zflac_batch* b) {
     if (!b) return;
