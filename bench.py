@@ -57,6 +57,7 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-md5", action="store_true", help="skip the device-MD5 leg")
     return ap.parse_args()
 
 
@@ -197,6 +198,28 @@ def main():
     samples_all, in_all, out_all = tot.samples, tot.input_bytes, tot.output_bytes
     ok = tot.errors == 0
 
+    # decode() also checks the STREAMINFO MD5 (src/zflac.zig:267-280): the same shard with
+    # the batched device MD5 (k_md5) after each decode, reported beside the headline
+    md5 = None
+    if not args.no_md5:
+        batch.close()
+        mb = zflac_amd.Batch(streams, device=local_rank, timing=True, device_md5=True)
+        md5_ms, tot_ms = [], []
+        for k in range(3):
+            mb.run()
+            if k:
+                md5_ms.append(mb.timings().md5_ms)
+                tot_ms.append(mb.timings().total_ms)
+        md5_ok = all(mb.info(i)[0] == 0 and mb.md5(i) is not None for i in range(len(streams)))
+        mb.close()
+        m_avg = float(np.mean(md5_ms))
+        md5 = {"kernel": "k_md5", "md5_ms": round(m_avg, 4), "all_match": md5_ok,
+               "decode_plus_md5_msps_rank0": round(samples_rank / ((elapsed / args.steps) + m_avg * 1e-3) / 1e6, 1),
+               "hashed_bytes_rank0": int(out_bytes),
+               "note": "one lane per stream (MD5 is a serial chain per stream); not in `value`"}
+        ok = ok and md5_ok
+        batch = None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(streams, args.cpu_seconds)
@@ -236,6 +259,7 @@ def main():
                           "walk": round(float(np.mean(walk_ms)), 4), "decode": round(dec_avg, 4),
                           "verify": round(float(np.mean(ver_ms)), 4)},
             "traffic_detail": pmc,
+            "device_md5": md5,
             "cpu_baseline": cpu,
             "gen_seconds": round(t_gen, 2),
         }
@@ -244,7 +268,8 @@ def main():
         print(json.dumps(line), flush=True)
         if errs:
             print("BIT-EXACTNESS FAILURES:", errs[:10], file=sys.stderr)
-    batch.close()
+    if batch is not None:
+        batch.close()
     if dist is not None:
         dist.destroy_process_group()
     if not ok:

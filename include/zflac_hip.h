@@ -10,7 +10,8 @@
  *
  * All decode work (frame sync scan, subframe decode, fixed/LPC rollback, wasted bits,
  * stereo decorrelation, left-justify, PCM pack-out) runs in HIP kernels on gfx950.
- * MD5 verification (src/zflac.zig:267-280) runs on the host over the PCM copied back.
+ * MD5 verification (src/zflac.zig:267-280) runs on the host over the PCM copied back,
+ * or, for batches created with ZFLAC_FLAG_DEVICE_MD5, in a HIP kernel (k_md5).
  * There is no CPU decode fallback: without a usable GPU every call returns
  * ZFLAC_E_DEVICE.
  *
@@ -79,6 +80,7 @@ typedef struct zflac_timings {
     uint64_t output_bytes;  /* PCM bytes written */
     uint64_t samples;       /* channel-samples written */
     double walk_ms;     /* subframe-start walk k_walk (2+ channels; runs before k_decode) */
+    double md5_ms;      /* batched STREAMINFO MD5 k_md5 (ZFLAC_FLAG_DEVICE_MD5), else 0 */
 } zflac_timings;
 
 typedef struct zflac_batch zflac_batch;
@@ -107,6 +109,10 @@ int zflac_hip_batch_run(zflac_batch *b);
 int zflac_hip_batch_info(zflac_batch *b, size_t i, zflac_info *info);
 /* Copy stream i's samples to host memory; verify_md5 != 0 checks STREAMINFO MD5. */
 int zflac_hip_batch_read(zflac_batch *b, size_t i, void *out, size_t out_bytes, int verify_md5);
+/* Device MD5 digest of stream i's samples as zflac hashes them (before left-justify,
+ * src/zflac.zig:267-277), computed by the last run when the batch was created with
+ * ZFLAC_FLAG_DEVICE_MD5; ZFLAC_E_INVALID_ARGUMENT otherwise. */
+int zflac_hip_batch_md5(zflac_batch *b, size_t i, uint8_t *digest16);
 /* Device pointer of stream i's samples (valid until the next run / destroy). */
 const void *zflac_hip_batch_device_samples(zflac_batch *b, size_t i);
 int zflac_hip_batch_timings(zflac_batch *b, zflac_timings *t);
@@ -116,6 +122,11 @@ void zflac_hip_batch_destroy(zflac_batch *b);
 /* Flags for zflac_hip_batch_create */
 #define ZFLAC_FLAG_TIMING 1        /* record HIP events around each kernel */
 #define ZFLAC_FLAG_FORCE_SLOW 2    /* skip the parallel fast path (testing the sequential path) */
+/* Verify every stream's STREAMINFO MD5 on the device after each run (one lane per
+ * stream: pays off for batches of many streams; a single long stream hashes faster on
+ * the host, which zflac_hip_read / zflac_hip_batch_read do without this flag). A
+ * mismatch makes the stream's result ZFLAC_E_INVALID_CHECKSUM (src/zflac.zig:279-280). */
+#define ZFLAC_FLAG_DEVICE_MD5 4
 
 const char *zflac_hip_error_name(int code);
 /* Number of HIP devices visible; 0 means every decode will fail with ZFLAC_E_DEVICE. */

@@ -105,6 +105,57 @@ def test_mixed_batch(gpu_ready):
     b.close()
 
 
+def _md5_pre_justify(v: np.ndarray, bps: int) -> bytes:
+    """hashlib MD5 of the samples as zflac hashes them (src/zflac.zig:267-277)."""
+    js = 16 - bps if 9 <= bps <= 15 else 32 - bps if 17 <= bps <= 31 else 0
+    x = v >> js
+    if v.dtype == np.int32 and (bps + 7) // 8 == 3:
+        b = x.astype("<i4").view(np.uint8).reshape(-1, 4)[:, :3]
+        return hashlib.md5(np.ascontiguousarray(b).tobytes()).digest()
+    return hashlib.md5(x.astype(v.dtype.newbyteorder("<")).tobytes()).digest()
+
+
+def _streaminfo_md5(flac: bytes) -> bytes:
+    return flac[26:42]  # 'fLaC', block header, then STREAMINFO bytes 18..33
+
+
+def test_device_md5_every_class(gpu_ready):
+    """k_md5 (ZFLAC_FLAG_DEVICE_MD5): every container/depth class (8..32-bit, justify
+    undone, 24-bit as 3 bytes), ragged lengths and unaligned stream bases in one batch;
+    digests equal hashlib over the oracle's pre-justify bytes and the STREAMINFO MD5;
+    a corrupted MD5 turns into InvalidChecksum."""
+    names = sorted(PARITY_CONFIGS)
+    streams = [synth.generate(**dict(PARITY_CONFIGS[n], seed=2000 + i)) for i, n in enumerate(names)]
+    datas = [s.flac for s in streams] + [_CASES["wrong_md5"][0]]
+    b = zflac_amd.Batch(datas, device_md5=True, timing=True)
+    b.run()
+    for i, data in enumerate(datas):
+        r = oracle.decode(data)
+        rc, _ = b.info(i)
+        assert errors.NAMES.get(rc) == r.error, (i, rc, r.error)
+        if r.error != "OK":
+            continue
+        dig = b.md5(i)
+        assert dig is not None, i
+        assert dig == _streaminfo_md5(data), i
+        assert dig == _md5_pre_justify(r.samples, r.bits_per_sample), i
+        d = b.read(i)  # device verdict stands in for the host hash
+        np.testing.assert_array_equal(d.samples.values, r.samples)
+    assert b.timings().md5_ms > 0
+    b.close()
+
+
+def test_device_md5_c5_shard(gpu_ready):
+    """C5-shaped members (32 frames, 131072 samples/ch), device MD5 against STREAMINFO."""
+    streams = synth.generate_many([synth.config_c5(i) for i in range(130)])
+    b = zflac_amd.Batch([s.flac for s in streams], device_md5=True)
+    b.run()
+    for i, s in enumerate(streams):
+        assert b.info(i)[0] == 0, i
+        assert b.md5(i) == _streaminfo_md5(s.flac), i
+    b.close()
+
+
 def test_batch_rerun_is_stable(gpu_ready):
     streams = [synth.generate(**synth.config_c5(i, n_frames=8)).flac for i in range(40)]
     b = zflac_amd.Batch(streams, timing=True)

@@ -27,7 +27,7 @@ class zflac_stream(ctypes.Structure):
 class zflac_timings(ctypes.Structure):
     _fields_ = [("scan_ms", ctypes.c_double), ("decode_ms", ctypes.c_double), ("verify_ms", ctypes.c_double),
                 ("total_ms", ctypes.c_double), ("frames", ctypes.c_uint64), ("input_bytes", ctypes.c_uint64),
-                ("output_bytes", ctypes.c_uint64), ("samples", ctypes.c_uint64), ("walk_ms", ctypes.c_double)]
+                ("output_bytes", ctypes.c_uint64), ("samples", ctypes.c_uint64), ("walk_ms", ctypes.c_double), ("md5_ms", ctypes.c_double)]
 
 
 # every symbol include/zflac_hip.h declares, with (restype, argtypes)
@@ -42,6 +42,7 @@ SIGNATURES = {
     "zflac_hip_batch_run": (ctypes.c_int, [_P]),
     "zflac_hip_batch_info": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(zflac_info)]),
     "zflac_hip_batch_read": (ctypes.c_int, [_P, ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.c_int]),
+    "zflac_hip_batch_md5": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_char_p]),
     "zflac_hip_batch_device_samples": (_P, [_P, ctypes.c_size_t]),
     "zflac_hip_batch_timings": (ctypes.c_int, [_P, ctypes.POINTER(zflac_timings)]),
     "zflac_hip_batch_size": (ctypes.c_size_t, [_P]),
@@ -53,6 +54,7 @@ SIGNATURES = {
 
 FLAG_TIMING = 1
 FLAG_FORCE_SLOW = 2
+FLAG_DEVICE_MD5 = 4
 
 _lib = None
 

@@ -99,7 +99,8 @@ class Batch:
     create -> run() (device-resident decode, repeatable) -> info(i) / read(i).
     """
 
-    def __init__(self, streams, device: int = 0, timing: bool = False, force_slow: bool = False):
+    def __init__(self, streams, device: int = 0, timing: bool = False, force_slow: bool = False,
+                 device_md5: bool = False):
         self._L = _lib.load()
         self._bufs = [bytes(s) for s in streams]
         arr = (_lib.zflac_stream * len(self._bufs))()
@@ -109,7 +110,8 @@ class Batch:
             self._keep.append(cb)
             arr[i].data = ctypes.cast(cb, ctypes.c_void_p)
             arr[i].len = len(b)
-        flags = (_lib.FLAG_TIMING if timing else 0) | (_lib.FLAG_FORCE_SLOW if force_slow else 0)
+        flags = ((_lib.FLAG_TIMING if timing else 0) | (_lib.FLAG_FORCE_SLOW if force_slow else 0)
+                 | (_lib.FLAG_DEVICE_MD5 if device_md5 else 0))
         self._h = ctypes.c_void_p()
         rc = self._L.zflac_hip_batch_create(arr, len(self._bufs), device, flags, ctypes.byref(self._h))
         self._keep = None  # the library copied the bytes to HBM
@@ -138,6 +140,12 @@ class Batch:
         errors.check(rc)
         return DecodedFLAC(inf.channels, inf.sample_rate, inf.bits_per_sample, Samples(_TAGS[inf.sample_kind], out))
 
+    def md5(self, i: int):
+        """Device MD5 digest of stream i (batches created with device_md5=True), else None."""
+        buf = ctypes.create_string_buffer(16)
+        rc = self._L.zflac_hip_batch_md5(self._h, i, buf)
+        return None if rc else buf.raw
+
     def timings(self):
         t = _lib.zflac_timings()
         rc = self._L.zflac_hip_batch_timings(self._h, ctypes.byref(t))
@@ -158,9 +166,12 @@ class Batch:
             pass
 
 
-def decode_many(streams, device: int = 0, verify_md5: bool = True):
-    """Decode independent streams in one batch; returns DecodedFLAC or exception per stream."""
-    b = Batch(streams, device)
+def decode_many(streams, device: int = 0, verify_md5: bool = True, device_md5: bool = True):
+    """Decode independent streams in one batch; returns DecodedFLAC or exception per stream.
+
+    With device_md5 the STREAMINFO MD5s are checked by k_md5 on the GPU (one lane per
+    stream) instead of on the host after the copy back."""
+    b = Batch(streams, device, device_md5=device_md5 and verify_md5)
     try:
         b.run()
         out = []

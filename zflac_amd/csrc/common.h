@@ -120,6 +120,24 @@ struct DecodeArgs {
     uint32_t* sub_start;  // [frame][MAX_CH]: bit offset of subframe c >= 1 (k_walk -> k_decode)
 };
 
+// One stream for k_md5 (md5.hip): the message is the decoded samples before left-justify,
+// rebuilt from the justified device samples (src/zflac.zig:267-280).
+enum Md5Mode : uint32_t {
+    MD5_RAW = 0,        // bytes as stored (8-bit, 16-bit, 32-bit containers with no justify)
+    MD5_S16_SHIFT = 1,  // i16 samples >> js (9..15-bit)
+    MD5_S32_SHIFT = 2,  // i32 samples >> js, 4 bytes each (25..31-bit)
+    MD5_S24 = 3,        // i32 samples >> js, 3 low bytes each (17..24-bit)
+};
+
+struct Md5Job {
+    const uint8_t* data;  // device samples of the stream
+    uint64_t n;           // samples
+    uint32_t mode;        // Md5Mode
+    uint32_t js;          // justify shift to undo
+    uint32_t width;       // message bytes per sample (1, 2, 3 or 4)
+    uint32_t pad_;
+};
+
 struct VerifyArgs {
     const StreamDesc* streams;
     uint32_t n_streams;

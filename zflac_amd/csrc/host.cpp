@@ -64,6 +64,7 @@ static hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_fram
     return launch_decode_k2_multi(a, max_frames, st);
 }
 hipError_t launch_verify(const VerifyArgs& a, uint32_t max_items, hipStream_t st);
+hipError_t launch_md5(const Md5Job* jobs, uint32_t n_jobs, uint32_t* digests, hipStream_t st);
 
 namespace {
 
@@ -247,6 +248,8 @@ struct StreamState {
     int err = 0;
     zflac_info info = {};
     const void* dev_samples = nullptr;  // device pointer of the decoded samples
+    int md5_dev = 0;                    // 0 not hashed on the device, 1 match, 2 mismatch
+    uint8_t md5_dig[16] = {};           // device digest (md5_dev != 0)
     std::unique_ptr<DevBuf<uint8_t>> override_out;
 };
 
@@ -288,6 +291,8 @@ struct zflac_batch {
     std::vector<std::unique_ptr<zflac::Class>> classes;
     hipEvent_t ev[8] = {};
     bool have_timing = false;
+    zflac::DevBuf<zflac::Md5Job> md5_jobs;
+    zflac::DevBuf<uint32_t> md5_dig;
     zflac_timings timings = {};
     ~zflac_batch() {
         classes.clear();
@@ -689,6 +694,8 @@ void finish_stream_sequential(zflac_batch* b, Class& C, uint32_t slot, const std
     s.info.bits_per_sample = (uint8_t)bps0;
 }
 
+void run_md5_device(zflac_batch* b, bool timing);
+
 void run_batch(zflac_batch* b) {
     ck(hipSetDevice(b->device));
     const bool timing = (b->flags & ZFLAC_FLAG_TIMING) != 0;
@@ -751,6 +758,10 @@ void run_batch(zflac_batch* b) {
         }
         frames += std::min(C.h_misc[0], C.cap);
     }
+    b->timings.md5_ms = 0;
+    if (b->flags & ZFLAC_FLAG_DEVICE_MD5) run_md5_device(b, timing && !b->classes.empty());
+    else
+        for (auto& s : b->streams) s.md5_dev = 0;
     b->timings.frames = frames;
     b->timings.input_bytes = in_bytes;
     b->timings.output_bytes = out_bytes;
@@ -799,6 +810,66 @@ bool md5_matches(const StreamState& s, const void* host_samples) {
     uint8_t dig[16];
     md.finish(dig);
     return std::memcmp(dig, s.si.md5, 16) == 0;
+}
+
+// STREAMINFO MD5 of every decoded stream on the device (k_md5, one lane per stream),
+// ZFLAC_FLAG_DEVICE_MD5. A mismatch becomes the stream's error, as decode() returns
+// InvalidChecksum (src/zflac.zig:279-280).
+void run_md5_device(zflac_batch* b, bool timing) {
+    std::vector<Md5Job> jobs;
+    std::vector<uint32_t> who;
+    for (size_t i = 0; i < b->streams.size(); i++) {
+        StreamState& s = b->streams[i];
+        s.md5_dev = 0;
+        if (s.err || !s.dev_samples) continue;
+        Md5Job j{};
+        j.data = static_cast<const uint8_t*>(s.dev_samples);
+        j.n = s.info.n_samples;
+        const uint32_t js = justify_of(s.si.bps);
+        j.js = js;
+        if (s.kind == 0) {
+            j.mode = MD5_RAW, j.width = 1;
+        } else if (s.kind == 1) {
+            j.mode = js ? MD5_S16_SHIFT : MD5_RAW, j.width = 2;
+        } else if ((s.si.bps + 7) / 8 * 8 == 24) {
+            j.mode = MD5_S24, j.width = 3;
+        } else {
+            j.mode = js ? MD5_S32_SHIFT : MD5_RAW, j.width = 4;
+        }
+        jobs.push_back(j);
+        who.push_back((uint32_t)i);
+    }
+    if (jobs.empty()) return;
+    // longest messages first: the lanes of a wave then run chains of similar length
+    std::vector<uint32_t> ord(jobs.size());
+    for (uint32_t k = 0; k < ord.size(); k++) ord[k] = k;
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+        return jobs[x].n * jobs[x].width > jobs[y].n * jobs[y].width;
+    });
+    std::vector<Md5Job> sorted(jobs.size());
+    for (size_t k = 0; k < ord.size(); k++) sorted[k] = jobs[ord[k]];
+    b->md5_jobs.alloc(sorted.size());
+    b->md5_dig.alloc(sorted.size() * 4);
+    ck(hipMemcpyAsync(b->md5_jobs.p, sorted.data(), sorted.size() * sizeof(Md5Job), hipMemcpyHostToDevice,
+                      b->stream));
+    if (timing) ck(hipEventRecord(b->ev[5], b->stream));
+    ck(launch_md5(b->md5_jobs.p, (uint32_t)sorted.size(), b->md5_dig.p, b->stream));
+    if (timing) ck(hipEventRecord(b->ev[6], b->stream));
+    std::vector<uint32_t> dig(sorted.size() * 4);
+    ck(hipMemcpyAsync(dig.data(), b->md5_dig.p, dig.size() * 4, hipMemcpyDeviceToHost, b->stream));
+    ck(hipStreamSynchronize(b->stream));
+    if (timing) {
+        float t = 0;
+        ck(hipEventElapsedTime(&t, b->ev[5], b->ev[6]));
+        b->timings.md5_ms = t;
+    }
+    for (size_t k = 0; k < ord.size(); k++) {
+        StreamState& s = b->streams[who[ord[k]]];
+        for (int w = 0; w < 4; w++)
+            for (int q = 0; q < 4; q++) s.md5_dig[4 * w + q] = (uint8_t)(dig[k * 4 + w] >> (8 * q));
+        s.md5_dev = std::memcmp(s.md5_dig, s.si.md5, 16) == 0 ? 1 : 2;
+        if (s.md5_dev == 2) s.err = E_INVALID_CHECKSUM;
+    }
 }
 
 int create_batch(const zflac_stream* streams, size_t n, int device, int flags, zflac_batch** out) {
@@ -935,7 +1006,16 @@ int zflac_hip_batch_read(zflac_batch* b, size_t i, void* out, size_t out_bytes, 
     } catch (const DeviceError&) {
         return E_DEVICE;
     }
-    if (verify_md5 && !md5_matches(s, out)) return E_INVALID_CHECKSUM;  // :279-280
+    // a device verdict stands in for the host hash (a mismatch is already s.err)
+    if (verify_md5 && !s.md5_dev && !md5_matches(s, out)) return E_INVALID_CHECKSUM;  // :279-280
+    return E_OK;
+}
+
+int zflac_hip_batch_md5(zflac_batch* b, size_t i, uint8_t* digest) {
+    if (!b || i >= b->streams.size() || !digest) return E_INVALID_ARGUMENT;
+    const StreamState& s = b->streams[i];
+    if (!s.md5_dev) return E_INVALID_ARGUMENT;
+    std::memcpy(digest, s.md5_dig, 16);
     return E_OK;
 }
 

@@ -1,0 +1,200 @@
+// md5.hip -- batched STREAMINFO MD5 of decoded streams on the device.
+//
+// zflac hashes the decoded samples before left-justify (src/zflac.zig:267-280): the whole
+// sample backing for 8/16/32-bit containers, 3 little-endian bytes per i32 for 24-bit
+// containers. The device buffers hold the samples after left-justify (done at pack-out),
+// so the message bytes are rebuilt on the fly: each sample is shifted back right by the
+// stream's justify amount (arithmetic, as the values were sign-extended before it).
+//
+// MD5 (RFC 1321) is a chain over 64-byte blocks, so one stream is one lane: a batch of
+// many streams fills waves, one long stream does not (the host keeps the CPU hash for
+// that case, see host.cpp). Per block: 16 message words from HBM (loaded one unit ahead
+// of the compression that uses them), 64 dependent rounds of ~5 VALU ops.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+
+namespace zflac {
+namespace {
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int s) { return __builtin_amdgcn_alignbit(x, x, 32 - s); }
+
+#define MD_F(x, y, z) ((z) ^ ((x) & ((y) ^ (z))))
+#define MD_G(x, y, z) ((y) ^ ((z) & ((x) ^ (y))))
+#define MD_H(x, y, z) ((x) ^ (y) ^ (z))
+#define MD_I(x, y, z) ((y) ^ ((x) | ~(z)))
+#define MD_R(f, a, b, c, d, k, t, s) a = (b) + rotl((a) + f(b, c, d) + m[k] + (t), s)
+
+__device__ __forceinline__ void compress(uint32_t st[4], const uint32_t m[16]) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+    MD_R(MD_F, a, b, c, d, 0, 0xd76aa478u, 7);  MD_R(MD_F, d, a, b, c, 1, 0xe8c7b756u, 12);
+    MD_R(MD_F, c, d, a, b, 2, 0x242070dbu, 17); MD_R(MD_F, b, c, d, a, 3, 0xc1bdceeeu, 22);
+    MD_R(MD_F, a, b, c, d, 4, 0xf57c0fafu, 7);  MD_R(MD_F, d, a, b, c, 5, 0x4787c62au, 12);
+    MD_R(MD_F, c, d, a, b, 6, 0xa8304613u, 17); MD_R(MD_F, b, c, d, a, 7, 0xfd469501u, 22);
+    MD_R(MD_F, a, b, c, d, 8, 0x698098d8u, 7);  MD_R(MD_F, d, a, b, c, 9, 0x8b44f7afu, 12);
+    MD_R(MD_F, c, d, a, b, 10, 0xffff5bb1u, 17); MD_R(MD_F, b, c, d, a, 11, 0x895cd7beu, 22);
+    MD_R(MD_F, a, b, c, d, 12, 0x6b901122u, 7); MD_R(MD_F, d, a, b, c, 13, 0xfd987193u, 12);
+    MD_R(MD_F, c, d, a, b, 14, 0xa679438eu, 17); MD_R(MD_F, b, c, d, a, 15, 0x49b40821u, 22);
+    MD_R(MD_G, a, b, c, d, 1, 0xf61e2562u, 5);  MD_R(MD_G, d, a, b, c, 6, 0xc040b340u, 9);
+    MD_R(MD_G, c, d, a, b, 11, 0x265e5a51u, 14); MD_R(MD_G, b, c, d, a, 0, 0xe9b6c7aau, 20);
+    MD_R(MD_G, a, b, c, d, 5, 0xd62f105du, 5);  MD_R(MD_G, d, a, b, c, 10, 0x02441453u, 9);
+    MD_R(MD_G, c, d, a, b, 15, 0xd8a1e681u, 14); MD_R(MD_G, b, c, d, a, 4, 0xe7d3fbc8u, 20);
+    MD_R(MD_G, a, b, c, d, 9, 0x21e1cde6u, 5);  MD_R(MD_G, d, a, b, c, 14, 0xc33707d6u, 9);
+    MD_R(MD_G, c, d, a, b, 3, 0xf4d50d87u, 14); MD_R(MD_G, b, c, d, a, 8, 0x455a14edu, 20);
+    MD_R(MD_G, a, b, c, d, 13, 0xa9e3e905u, 5); MD_R(MD_G, d, a, b, c, 2, 0xfcefa3f8u, 9);
+    MD_R(MD_G, c, d, a, b, 7, 0x676f02d9u, 14); MD_R(MD_G, b, c, d, a, 12, 0x8d2a4c8au, 20);
+    MD_R(MD_H, a, b, c, d, 5, 0xfffa3942u, 4);  MD_R(MD_H, d, a, b, c, 8, 0x8771f681u, 11);
+    MD_R(MD_H, c, d, a, b, 11, 0x6d9d6122u, 16); MD_R(MD_H, b, c, d, a, 14, 0xfde5380cu, 23);
+    MD_R(MD_H, a, b, c, d, 1, 0xa4beea44u, 4);  MD_R(MD_H, d, a, b, c, 4, 0x4bdecfa9u, 11);
+    MD_R(MD_H, c, d, a, b, 7, 0xf6bb4b60u, 16); MD_R(MD_H, b, c, d, a, 10, 0xbebfbc70u, 23);
+    MD_R(MD_H, a, b, c, d, 13, 0x289b7ec6u, 4); MD_R(MD_H, d, a, b, c, 0, 0xeaa127fau, 11);
+    MD_R(MD_H, c, d, a, b, 3, 0xd4ef3085u, 16); MD_R(MD_H, b, c, d, a, 6, 0x04881d05u, 23);
+    MD_R(MD_H, a, b, c, d, 9, 0xd9d4d039u, 4);  MD_R(MD_H, d, a, b, c, 12, 0xe6db99e5u, 11);
+    MD_R(MD_H, c, d, a, b, 15, 0x1fa27cf8u, 16); MD_R(MD_H, b, c, d, a, 2, 0xc4ac5665u, 23);
+    MD_R(MD_I, a, b, c, d, 0, 0xf4292244u, 6);  MD_R(MD_I, d, a, b, c, 7, 0x432aff97u, 10);
+    MD_R(MD_I, c, d, a, b, 14, 0xab9423a7u, 15); MD_R(MD_I, b, c, d, a, 5, 0xfc93a039u, 21);
+    MD_R(MD_I, a, b, c, d, 12, 0x655b59c3u, 6); MD_R(MD_I, d, a, b, c, 3, 0x8f0ccc92u, 10);
+    MD_R(MD_I, c, d, a, b, 10, 0xffeff47du, 15); MD_R(MD_I, b, c, d, a, 1, 0x85845dd1u, 21);
+    MD_R(MD_I, a, b, c, d, 8, 0x6fa87e4fu, 6);  MD_R(MD_I, d, a, b, c, 15, 0xfe2ce6e0u, 10);
+    MD_R(MD_I, c, d, a, b, 6, 0xa3014314u, 15); MD_R(MD_I, b, c, d, a, 13, 0x4e0811a1u, 21);
+    MD_R(MD_I, a, b, c, d, 4, 0xf7537e82u, 6);  MD_R(MD_I, d, a, b, c, 11, 0xbd3af235u, 10);
+    MD_R(MD_I, c, d, a, b, 2, 0x2ad7d2bbu, 15); MD_R(MD_I, b, c, d, a, 9, 0xeb86d391u, 21);
+    st[0] += a;
+    st[1] += b;
+    st[2] += c;
+    st[3] += d;
+}
+
+// Message word from a raw little-endian word of the sample buffer (modes RAW, S16, S32).
+template <int MODE>
+__device__ __forceinline__ uint32_t unjustify_word(uint32_t r, uint32_t js) {
+    if constexpr (MODE == MD5_S16_SHIFT) {
+        const uint32_t lo = (uint32_t)((int32_t)(int16_t)(r & 0xffffu) >> js) & 0xffffu;
+        const uint32_t hi = (uint32_t)(((int32_t)r >> 16) >> js);
+        return lo | (hi << 16);
+    } else if constexpr (MODE == MD5_S32_SHIFT) {
+        return (uint32_t)((int32_t)r >> js);
+    } else {
+        return r;
+    }
+}
+
+// Byte v of the hashed message (tail blocks only).
+__device__ uint32_t message_byte(const Md5Job& j, uint64_t v) {
+    switch (j.mode) {
+        case MD5_RAW: return j.data[v];
+        case MD5_S16_SHIFT: {
+            const int16_t x = reinterpret_cast<const int16_t*>(j.data)[v >> 1];
+            return ((uint32_t)((int32_t)x >> j.js) >> (8 * (v & 1))) & 0xffu;
+        }
+        case MD5_S32_SHIFT: {
+            const int32_t x = reinterpret_cast<const int32_t*>(j.data)[v >> 2];
+            return ((uint32_t)(x >> j.js) >> (8 * (v & 3))) & 0xffu;
+        }
+        default: {  // MD5_S24: 3 bytes per i32 sample
+            const int32_t x = reinterpret_cast<const int32_t*>(j.data)[v / 3];
+            return ((uint32_t)(x >> j.js) >> (8 * (uint32_t)(v % 3))) & 0xffu;
+        }
+    }
+}
+
+constexpr int UNIT_WORDS = 64;  // raw dwords per unit: 4 blocks, or 3 blocks of 24-bit samples
+
+// The full units of one stream: 256 raw bytes each, loaded one unit (3-4 blocks of
+// compression, several microseconds) ahead of their use. Returns message bytes hashed.
+template <int MODE>
+__device__ __forceinline__ uint64_t hash_units(const Md5Job& j, uint32_t st[4]) {
+    constexpr uint64_t MSG_PER_UNIT = MODE == MD5_S24 ? 192 : 256;
+    const uint64_t L = j.n * (uint64_t)j.width;
+    const uint64_t nu = L / MSG_PER_UNIT;
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(j.data) & 3);
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(j.data) & ~(uintptr_t)3);
+    uint32_t cur[UNIT_WORDS + 1], nxt[UNIT_WORDS + 1];
+    auto load = [&](uint64_t u, uint32_t* r) {
+        const uint32_t* q = p + u * UNIT_WORDS;
+#pragma unroll
+        for (int i = 0; i < UNIT_WORDS; i++) r[i] = __builtin_nontemporal_load(q + i);
+        // the dword after the unit carries its last bytes when the base is unaligned
+        r[UNIT_WORDS] = (MODE != MD5_S24 && sh) ? __builtin_nontemporal_load(q + UNIT_WORDS) : 0u;
+    };
+    if (nu) load(0, cur);
+    for (uint64_t u = 0; u < nu; u++) {
+        if (u + 1 < nu) load(u + 1, nxt);
+        uint32_t m[16];
+        if constexpr (MODE == MD5_S24) {
+#pragma unroll
+            for (int blk = 0; blk < 3; blk++) {
+#pragma unroll
+                for (int w = 0; w < 16; w++) {
+                    // 4 samples -> 3 words: x0|x1<<24, x1>>8|x2<<16, x2>>16|x3<<8
+                    const int g = blk * 16 + w, ph = g % 3, s0 = (g / 3) * 4 + ph;
+                    const uint32_t x0 = (uint32_t)((int32_t)cur[s0] >> j.js) & 0xffffffu;
+                    const uint32_t x1 = (uint32_t)((int32_t)cur[s0 + 1] >> j.js) & 0xffffffu;
+                    m[w] = ph == 0 ? (x0 | (x1 << 24)) : ph == 1 ? ((x0 >> 8) | (x1 << 16)) : ((x0 >> 16) | (x1 << 8));
+                }
+                compress(st, m);
+            }
+        } else {
+#pragma unroll
+            for (int blk = 0; blk < 4; blk++) {
+#pragma unroll
+                for (int w = 0; w < 16; w++)
+                    m[w] = unjustify_word<MODE>(
+                        __builtin_amdgcn_alignbyte(cur[blk * 16 + w + 1], cur[blk * 16 + w], sh), j.js);
+                compress(st, m);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i <= UNIT_WORDS; i++) cur[i] = nxt[i];
+    }
+    return nu * MSG_PER_UNIT;
+}
+
+__global__ __launch_bounds__(64) void k_md5(const Md5Job* __restrict__ jobs, uint32_t n_jobs,
+                                            uint32_t* __restrict__ digests) {
+    const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+    if (t >= n_jobs) return;
+    const Md5Job j = jobs[t];
+    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    const uint64_t L = j.n * (uint64_t)j.width;  // message bytes
+    uint64_t done;                                // message bytes hashed by the unit loop
+    switch (j.mode) {
+        case MD5_RAW: done = hash_units<MD5_RAW>(j, st); break;
+        case MD5_S16_SHIFT: done = hash_units<MD5_S16_SHIFT>(j, st); break;
+        case MD5_S32_SHIFT: done = hash_units<MD5_S32_SHIFT>(j, st); break;
+        default: done = hash_units<MD5_S24>(j, st); break;
+    }
+    // tail: remaining message bytes, 0x80, zero fill, 64-bit little-endian bit length
+    uint32_t m[16];
+    const uint64_t r = L - done;
+    const uint32_t tb = (uint32_t)((r + 8) / 64 + 1);
+    const uint64_t bits = L * 8;
+    for (uint32_t b = 0; b < tb; b++) {
+        for (int w = 0; w < 16; w++) {
+            uint32_t word = 0;
+            for (int q = 0; q < 4; q++) {
+                const uint64_t o = (uint64_t)b * 64 + w * 4 + q;  // offset from `done`
+                uint32_t byte;
+                if (o < r) byte = message_byte(j, done + o);
+                else if (o == r) byte = 0x80u;
+                else if (b + 1 == tb && w >= 14) byte = (uint32_t)(bits >> (8 * ((w - 14) * 4 + q))) & 0xffu;
+                else byte = 0;
+                word |= byte << (8 * q);
+            }
+            m[w] = word;
+        }
+        compress(st, m);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) digests[(uint64_t)t * 4 + i] = st[i];
+}
+
+}  // namespace
+
+hipError_t launch_md5(const Md5Job* jobs, uint32_t n_jobs, uint32_t* digests, hipStream_t st) {
+    if (!n_jobs) return hipSuccess;
+    hipLaunchKernelGGL(k_md5, dim3((n_jobs + 63) / 64), dim3(64), 0, st, jobs, n_jobs, digests);
+    return hipGetLastError();
+}
+
+}  // namespace zflac
