@@ -111,6 +111,32 @@ def cases():
     out["partition_order_not_dividing"] = (
         _base(fault_frame=1, fault_kind=5, block_size=4095, partition_order=0, n_samples=4095 * 4).flac,
         "OutOfDomain")
+    # STREAMINFO max block size / max frame size are never used (faulty/01, faulty/02)
+    def _si_max_block(v):
+        def f(b, o):
+            b[o + 2], b[o + 3] = (v >> 8) & 0xFF, v & 0xFF
+        return f
+
+    def _si_max_frame(v):
+        def f(b, o):
+            b[o + 7], b[o + 8], b[o + 9] = (v >> 16) & 0xFF, (v >> 8) & 0xFF, v & 0xFF
+        return f
+
+    out["wrong_max_blocksize"] = (_set_si_field(st.flac, _si_max_block(16)), "OK")  # faulty/01
+    out["wrong_max_framesize"] = (_set_si_field(st.flac, _si_max_frame(1)), "OK")  # faulty/02
+    # a PADDING block ahead of STREAMINFO (faulty/07): the metadata loop takes any order (:228-265)
+    out["streaminfo_not_first"] = (b"fLaC" + bytes([0x01, 0, 0, 4, 0, 0, 0, 0]) + st.flac[4:], "OK")
+    # a VORBIS_COMMENT block whose content is garbage is skipped unread (faulty/10, :248-250)
+    si_end = streaminfo_offset(st.flac) + 34
+    vc = bytes([0x04 | (st.flac[4] & 0x80), 0, 0, 9]) + b"\xff\xff\xff\x7fjunk\x00"
+    out["invalid_vorbis_comment"] = (st.flac[:4] + bytes([st.flac[4] & 0x7F]) + st.flac[5:si_end] + vc
+                                     + st.flac[si_end:], "OK")
+    # uncommon 16-bit block size 0xFFFF -> 65536 is refused (faulty/08, :358-361); the CRC-8
+    # byte is not rewritten (zflac never reads it back before failing)
+    h = bytearray(st.flac[fo[2]:fo[2] + 5])
+    h[2] = (7 << 4) | (h[2] & 0x0F)
+    out["blocksize_65536_frame2"] = (st.flac[:fo[2]] + bytes(h) + b"\xff\xff" + st.flac[fo[2] + 5:],
+                                     "InvalidFrameHeader")
     # a last frame of one sample is legal (:405)
     out["blocksize1_last"] = (_base(n_samples=4096 * 3 + 1).flac, "OK")
     del n

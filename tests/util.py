@@ -84,6 +84,14 @@ PARITY_CONFIGS = {
                             rice_k=26, rice2=1, noise_lsb=float(2 ** 29), tone_amp=0.0),
     "longcodes16_k3": dict(channels=2, bps=16, stereo_mode=10, order=8, precision=12, block_size=4096,
                            n_samples=4096 * 2, rice_k=3, partition_order=2, noise_lsb=300.0),
+    # the reference's uncommon suite (tests/std_uncommon.zig:37-54)
+    "uncommon_15bit": dict(channels=2, bps=15, stereo_mode=10, order=8, block_size=4096, n_samples=4096 * 3),
+    "uncommon_768khz": dict(channels=2, bps=24, sample_rate=768000, order=12, precision=14, block_size=4096,
+                            n_samples=4096 * 3, noise_lsb=64.0),
+    "uncommon_block65535": dict(channels=2, bps=16, stereo_mode=10, order=8, block_size=65535,
+                                n_samples=65535 * 2 + 100),
+    "uncommon_po15": dict(channels=1, bps=16, predictor=2, order=1, block_size=32768, partition_order=15,
+                          n_samples=32768 * 2),
     "variable_blocking": dict(channels=2, bps=16, variable_blocking=1, block_size=3000, n_samples=20000),
     "unknown_total": dict(channels=2, bps=16, write_total=0, block_size=4096, n_samples=4096 * 3 + 7),
     "silence_constant": dict(channels=2, bps=16, stereo_mode=1, silence_every=2, block_size=4096,
