@@ -272,8 +272,16 @@ struct Class {
     DevBuf<uint32_t> c_stream, c_info, c_rate, sub;
     DevBuf<int32_t> c_err;
     DevBuf<uint8_t> dummy;  // sink of masked-off packed stores (64 lanes x 32 B)
-    std::vector<uint32_t> h_status;
-    uint32_t h_misc[4] = {0, 0, 0, 0};  // [0] n_frames, [1] overflow
+    // pinned host mirror, so the per-run read-backs are plain DMA on the batch stream:
+    // [0] n_frames, [1] overflow, [2..3] unused, then one status word per member
+    struct Pinned {
+        uint32_t* p = nullptr;
+        ~Pinned() {
+            if (p) (void)hipHostFree(p);
+        }
+    } pin;
+    uint32_t* h_misc = nullptr;
+    uint32_t* h_status = nullptr;
 };
 
 }  // namespace
@@ -407,7 +415,11 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     C.misc.alloc(4);
     C.dummy.alloc(DUMMY_BYTES + PROBE_BYTES);
     C.status.alloc(C.members.size());
-    C.h_status.assign(C.members.size(), 0);
+    ck(hipHostMalloc(reinterpret_cast<void**>(&C.pin.p), (4 + C.members.size()) * sizeof(uint32_t),
+                     hipHostMallocDefault));
+    std::memset(C.pin.p, 0, (4 + C.members.size()) * sizeof(uint32_t));
+    C.h_misc = C.pin.p;
+    C.h_status = C.pin.p + 4;
     C.cap = (uint32_t)std::min<uint64_t>(est_frames + C.chunks.size() * 2 + 1024, 0x7FFFFFFFull);
 }
 
@@ -499,7 +511,7 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     va.status = C.status.p;
     ck(launch_verify(va, C.cap, st));
     if (timing_last) ck(hipEventRecord(b->ev[3], st));
-    ck(hipMemcpyAsync(C.h_status.data(), C.status.p, C.members.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    ck(hipMemcpyAsync(C.h_status, C.status.p, C.members.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     ck(hipMemcpyAsync(C.h_misc, C.misc.p, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
 }
 
