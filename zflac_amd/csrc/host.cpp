@@ -896,7 +896,9 @@ int create_batch(const zflac_stream* streams, size_t n, int device, int flags, z
     try {
         ck(hipSetDevice(device));
         ck(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
-        for (auto& e : b->ev) ck(hipEventCreate(&e));
+        // timing-only events: no system-scope fence (cache writeback + invalidate) at each
+        // record, which would otherwise slow the kernel after it
+        for (auto& e : b->ev) ck(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         b->streams.resize(n);
         for (size_t i = 0; i < n; i++) {
             if (!streams[i].data && streams[i].len) return E_INVALID_ARGUMENT;
