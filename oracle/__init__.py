@@ -68,13 +68,14 @@ def decode(data: bytes, flavor: str = "checked") -> OracleResult:
     lib = _lib(flavor)
     r = _Result()
     err = lib.zfo_decode(data, len(data), ctypes.byref(r))
-    if err:
-        return OracleResult(err)
     try:
+        if err and not r.samples:
+            return OracleResult(err)
+        # OK, or InvalidChecksum with the decoded (justified) samples kept for comparison
         dt = np.dtype(_KIND_DTYPE[r.sample_kind])
         nbytes = r.n_samples * dt.itemsize
         arr = np.frombuffer(ctypes.string_at(r.samples, nbytes), dtype=dt).copy() if nbytes else np.zeros(0, dt)
-        return OracleResult(0, r.channels, r.sample_rate, r.bits_per_sample, arr)
+        return OracleResult(err, r.channels, r.sample_rate, r.bits_per_sample, arr)
     finally:
         lib.zfo_free(ctypes.byref(r))
 

@@ -53,7 +53,7 @@ typedef struct zfo_result {
     uint8_t _pad;
     uint32_t sample_rate;     /* DecodedFLAC.sample_rate     src/zflac.zig:20 */
     uint64_t n_samples;       /* samples.len (channel-samples, interleaved) */
-    void *samples;            /* malloc'd; free with zfo_free */
+    void *samples;            /* malloc'd (kept on InvalidChecksum too); free with zfo_free */
 } zfo_result;
 
 /* Full decode() semantics: signature, metadata walk, frames, MD5 verification,

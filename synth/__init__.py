@@ -32,6 +32,8 @@ class _Config(ctypes.Structure):
         ("tone_amp", ctypes.c_double), ("noise_lsb", ctypes.c_double), ("stereo_corr", ctypes.c_double),
         ("fault_frame", ctypes.c_int), ("fault_kind", ctypes.c_int),
         ("n_samples", ctypes.c_uint64), ("seed", ctypes.c_uint64),
+        ("dual_mono_every", ctypes.c_int), ("dual_mono_offset", ctypes.c_int), ("const_side", ctypes.c_int),
+        ("plant_sync_every", ctypes.c_int), ("allow_side_overflow", ctypes.c_int),
     ]
 
 
@@ -63,6 +65,9 @@ def _load():
         lib.flacgen_default_config.argtypes = [ctypes.POINTER(_Config)]
         lib.flacgen_generate.argtypes = [ctypes.POINTER(_Config), ctypes.POINTER(_Output)]
         lib.flacgen_generate.restype = ctypes.c_int
+        lib.flacgen_generate_pcm.argtypes = [ctypes.POINTER(_Config), ctypes.POINTER(ctypes.c_int32), ctypes.c_uint64,
+                                             ctypes.POINTER(_Output)]
+        lib.flacgen_generate_pcm.restype = ctypes.c_int
         lib.flacgen_free.argtypes = [ctypes.POINTER(_Output)]
         _lib = lib
     return _lib
@@ -85,7 +90,9 @@ def default_config() -> dict:
     return {name: getattr(c, name) for name, _ in _Config._fields_}
 
 
-def generate(**overrides) -> Stream:
+def generate(pcm: np.ndarray | None = None, **overrides) -> Stream:
+    """Encode the seeded synthetic signal, or `pcm` (interleaved int32, unjustified,
+    `channels` per sample; n_samples is then taken from its length)."""
     lib = _load()
     c = _Config()
     lib.flacgen_default_config(ctypes.byref(c))
@@ -96,7 +103,13 @@ def generate(**overrides) -> Stream:
         setattr(c, k, v)
         cfg[k] = v
     out = _Output()
-    rc = lib.flacgen_generate(ctypes.byref(c), ctypes.byref(out))
+    if pcm is None:
+        rc = lib.flacgen_generate(ctypes.byref(c), ctypes.byref(out))
+    else:
+        src = np.ascontiguousarray(pcm, dtype=np.int32)
+        cfg["n_samples"] = src.size // max(1, c.channels)
+        rc = lib.flacgen_generate_pcm(ctypes.byref(c), src.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), src.size,
+                                      ctypes.byref(out))
     if rc != 0:
         raise ValueError(f"flacgen_generate failed ({rc}) for {cfg}")
     try:

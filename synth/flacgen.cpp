@@ -1,9 +1,11 @@
 // flacgen.cpp -- seeded synthetic FLAC writer. See flacgen.h.
 //
 // Format written per RFC 9639; choices that matter for zflac parity:
-//  * side channels never use CONSTANT subframes (zflac reads `bits_per_sample`
-//    bits for them, src/zflac.zig:447, the RFC reads bps+1);
-//  * side channels always fit the SampleType container (src/zflac.zig:494,537,558,564);
+//  * side channels use CONSTANT subframes only on request (`const_side`): zflac reads
+//    `bits_per_sample` bits for them (src/zflac.zig:447), the RFC reads bps+1; both widths
+//    can be written so the quirk and its mismatch with RFC encoders are testable;
+//  * side channels fit the SampleType container (src/zflac.zig:494,537,558,564) unless
+//    `allow_side_overflow` asks for an out-of-domain stream;
 //  * every LPC partial sum is checked against the InterType width in the order zflac
 //    accumulates it (src/zflac.zig:527-532), so Debug zflac would not trap;
 //  * the block size is always divisible by 2^partition_order (src/zflac.zig:623-632).
@@ -105,6 +107,7 @@ struct Encoder {
     uint64_t partition_counter = 0;
     uint64_t subframe_counter = 0;
     int fault = 0;  // active fault kind for the frame being written
+    bool force_verbatim = false;  // the subframe being written must be VERBATIM (planted sync)
 
     explicit Encoder(const flacgen_config& cfg) : c(cfg) {
         int aligned = (cfg.bps + 7) / 8 * 8;
@@ -266,6 +269,19 @@ struct Encoder {
         return true;
     }
 
+    template <typename H>
+    void write_fixed_or_verbatim(BitWriter& bw, const std::vector<int64_t>& u, int cbps, int bs, H& header) {
+        std::vector<int64_t> q = {2, -1}, r;
+        if (bs > 2 && predict(u, 2, q, 0, r)) {
+            header(10);
+            for (int i = 0; i < 2; i++) bw.put_signed(u[i], cbps);
+            write_residual(bw, r, bs, 2);
+            return;
+        }
+        header(1);
+        for (int i = 0; i < bs; i++) bw.put_signed(u[i], cbps);
+    }
+
     // ---- one subframe --------------------------------------------------------
     // v: the channel samples (after stereo transform), ubps: its coded width
     void write_subframe(BitWriter& bw, const std::vector<int64_t>& v, int ubps, bool side, int bs) {
@@ -297,17 +313,42 @@ struct Encoder {
                 bw.put(0, 1);
             }
         };
-        // CONSTANT: zflac reads `bits_per_sample - wasted` bits (not the side width)
-        const int const_bits = (ubps - (side ? 1 : 0)) - wasted;
-        if (all_equal && !side && const_bits > 0 && fits(u[0], const_bits)) {
+        // CONSTANT: zflac reads `bits_per_sample - wasted` bits, not the side width (:447);
+        // an RFC encoder writes the side width (const_side == 2)
+        const int const_bits = (ubps - (side && c.const_side != 2 ? 1 : 0)) - wasted;
+        if (all_equal && !force_verbatim && (!side || c.const_side) && const_bits > 0 && fits(u[0], const_bits)) {
             header(0);
             bw.put_signed(u[0], const_bits);
             return;
         }
-        const bool verbatim = c.predictor == FG_VERBATIM ||
+        const bool verbatim = force_verbatim || c.predictor == FG_VERBATIM ||
                               (c.verbatim_every > 0 && (sf_index % (uint64_t)c.verbatim_every) == 0);
         if (!verbatim) {
             int order = std::min(c.order, bs);
+            if (c.predictor == FG_LPC && order >= 1 && (fault == 7 || fault == 8)) {
+                // largest coefficients of the precision, shift 15: sum |c| * 2^(SB-1) exceeds
+                // what the fast path proves safe; kind 8 keeps overflowing sums
+                const int prec = c.precision;
+                std::vector<int64_t> q(order, (int64_t(1) << (prec - 1)) - 1), r;
+                const int shift = 15;
+                if (!predict(u, order, q, shift, r)) {
+                    if (fault == 7) return write_fixed_or_verbatim(bw, u, cbps, bs, header);
+                    r.assign(bs - order, 0);
+                    for (int i = order; i < bs; i++) {
+                        __int128 p = 0;
+                        for (int o = 0; o < order; o++) p += (__int128)u[i - order + o] * q[order - 1 - o];
+                        const __int128 res = (__int128)u[i] - (p >> shift);
+                        r[i - order] = fits((int64_t)res, ibits) && res == (__int128)(int64_t)res ? (int64_t)res : 0;
+                    }
+                }
+                header(31 + order);
+                for (int i = 0; i < order; i++) bw.put_signed(u[i], cbps);
+                bw.put(prec - 1, 4);
+                bw.put(shift, 5);
+                for (int j = 0; j < order; j++) bw.put_signed(q[j], prec);
+                write_residual(bw, r, bs, order);
+                return;
+            }
             if (c.predictor == FG_LPC && order >= 1) {
                 for (int prec = c.precision; prec >= 1; prec--) {
                     std::vector<int64_t> q, r;
@@ -383,6 +424,24 @@ int depth_code(int bps) {
     }
 }
 
+// Frame header with CRC-8 (RFC 9639 11.21; parsed by zflac at src/zflac.zig:343-407)
+std::vector<uint8_t> frame_header(const flacgen_config& c, size_t f, int bs, int chan_code, uint64_t sample_no) {
+    int bx, rx, rv;
+    std::vector<uint8_t> h;
+    h.push_back(0xFF);
+    h.push_back(c.variable_blocking ? 0xF9 : 0xF8);
+    const int bsc = block_size_code(bs, bx);
+    const int rc = rate_code(c.sample_rate, c.rate_code_mode, rx, rv);
+    h.push_back((uint8_t)((bsc << 4) | rc));
+    h.push_back((uint8_t)((chan_code << 4) | (depth_code(c.bps) << 1)));
+    put_utf8_number(h, c.variable_blocking ? sample_no : (uint64_t)f);
+    if (bx == 8) h.push_back((uint8_t)(bs - 1));
+    if (bx == 16) { h.push_back((uint8_t)((bs - 1) >> 8)); h.push_back((uint8_t)(bs - 1)); }
+    if (rx == 16) { h.push_back((uint8_t)(rv >> 8)); h.push_back((uint8_t)rv); }
+    h.push_back(crc8(h.data(), h.size()));
+    return h;
+}
+
 struct Synth {
     // sum of sinusoids (recursive oscillators) + first-order coloured noise
     struct Osc { double c, s, cr, sr, amp; };
@@ -439,13 +498,16 @@ void flacgen_default_config(flacgen_config* c) {
     c->fault_frame = -1;
 }
 
-int flacgen_generate(const flacgen_config* cfg, flacgen_output* out) {
+static int generate_impl(const flacgen_config* cfg, const int32_t* ext_pcm, flacgen_output* out) {
     std::memset(out, 0, sizeof(*out));
     const flacgen_config& c = *cfg;
     if (c.channels < 1 || c.channels > 8 || c.bps < 4 || c.bps > 32 || c.block_size < 16 || c.block_size > 65535)
         return -1;
     if (c.predictor == FG_LPC && (c.order < 1 || c.order > 32 || c.precision < 1 || c.precision > 15)) return -1;
     if (c.predictor == FG_FIXED && (c.order < 0 || c.order > 4)) return -1;
+    if (c.plant_sync_every > 0 && ((c.bps != 8 && c.bps != 16 && c.bps != 24) || c.wasted_bits ||
+                                   (c.channels == 2 && c.stereo_mode != 1)))
+        return -1;  // the planted header must sit byte-aligned in a VERBATIM channel-0 subframe
     Encoder enc(c);
     const int C = c.channels;
     const int sig_bits = c.bps - c.wasted_bits;  // significant bits
@@ -481,15 +543,18 @@ int flacgen_generate(const flacgen_config* cfg, flacgen_output* out) {
     uint32_t min_frame = ~0u, max_frame = 0;
     int min_block = 65535, max_block = 0;
     uint64_t sample_no = 0;
-    int bx, rx, rv;
-    const int depthc = depth_code(c.bps);
 
     for (size_t f = 0; f < blocks.size(); f++) {
         const int bs = blocks[f];
         // --- synthesize -----------------------------------------------------
         std::vector<std::vector<int64_t>> x(C, std::vector<int64_t>(bs));
         const bool silent0 = c.silence_every > 0 && (f % (size_t)c.silence_every) == 0;
+        const bool dual = C >= 2 && c.dual_mono_every > 0 && (f % (size_t)c.dual_mono_every) == (size_t)c.dual_mono_every - 1;
         for (int i = 0; i < bs; i++) {
+            if (ext_pcm) {
+                for (int ch = 0; ch < C; ch++) x[ch][i] = ext_pcm[(sample_no + i) * C + ch];
+                continue;
+            }
             double base = syn[0].tone() * fs + syn[0].noise() * c.noise_lsb;
             for (int ch = 0; ch < C; ch++) {
                 double v;
@@ -498,8 +563,28 @@ int flacgen_generate(const flacgen_config* cfg, flacgen_output* out) {
                 int64_t q = std::llround(v);
                 q = std::max(smin, std::min(smax, q));
                 if (ch == 0 && silent0) q = 0;
+                if (ch == 1 && dual) q = std::max(smin, std::min(smax, x[0][i] / (int64_t(1) << c.wasted_bits) - c.dual_mono_offset));
                 x[ch][i] = q * (int64_t(1) << c.wasted_bits);
             }
+        }
+        // planted false sync: channel 0 (VERBATIM, byte-aligned samples) carries a copy of
+        // this frame's own header, CRC-8 included, from sample bs / 2 on
+        const bool plant = c.plant_sync_every > 0 && (f % (size_t)c.plant_sync_every) == (size_t)c.plant_sync_every - 1;
+        if (plant) {
+            const std::vector<uint8_t> h = frame_header(c, f, bs, C == 1 ? 0 : C - 1, sample_no);
+            const int B = c.bps / 8;
+            const int i0 = bs / 2;
+            const int n = ((int)h.size() + B - 1) / B;
+            if (i0 < 1 || i0 + n > bs) return -1;
+            for (int j = 0; j < n; j++) {
+                uint64_t v = 0;
+                for (int b = 0; b < B; b++) {
+                    const size_t k = (size_t)j * B + b;
+                    v = (v << 8) | (k < h.size() ? h[k] : 0x55);
+                }
+                x[0][i0 + j] = (int64_t)(v << (64 - 8 * B)) >> (64 - 8 * B);
+            }
+            x[0][i0 - 1] |= 1;  // no wasted bits: the samples stay byte-aligned
         }
         for (int i = 0; i < bs; i++)
             for (int ch = 0; ch < C; ch++) {
@@ -520,7 +605,7 @@ int flacgen_generate(const flacgen_config* cfg, flacgen_output* out) {
                 ok = true;
                 for (int i = 0; i < bs; i++) {
                     int64_t L = x[0][i], R = x[1][i], S = L - R;
-                    if (mode != 1 && !fits(S, enc.sbits)) ok = false;
+                    if (mode != 1 && !fits(S, enc.sbits) && !c.allow_side_overflow) ok = false;
                     if (mode == 1) { s[0][i] = L; s[1][i] = R; }
                     else if (mode == 8) { s[0][i] = L; s[1][i] = S; }
                     else if (mode == 9) { s[0][i] = S; s[1][i] = R; }
@@ -548,25 +633,17 @@ int flacgen_generate(const flacgen_config* cfg, flacgen_output* out) {
             if (mode == 8 || mode == 10) { ubps[1] = c.bps + 1; side[1] = true; }
             if (mode == 9) { ubps[0] = c.bps + 1; side[0] = true; }
         }
+        if (c.fault_kind == 6 && (int)f == c.fault_frame)  // decorrelation overflow (stereo)
+            for (int i = 0; i < bs; i++) sub[0][i] = (int64_t(1) << (enc.sbits - 1)) - 1;
         // --- header -----------------------------------------------------------
-        std::vector<uint8_t> h;
-        h.push_back(0xFF);
-        h.push_back(c.variable_blocking ? 0xF9 : 0xF8);
-        int bsc = block_size_code(bs, bx);
-        int rc = rate_code(c.sample_rate, c.rate_code_mode, rx, rv);
-        h.push_back((uint8_t)((bsc << 4) | rc));
-        h.push_back((uint8_t)((chan_code << 4) | (depthc << 1)));
-        put_utf8_number(h, c.variable_blocking ? sample_no : (uint64_t)f);
-        if (bx == 8) h.push_back((uint8_t)(bs - 1));
-        if (bx == 16) { h.push_back((uint8_t)((bs - 1) >> 8)); h.push_back((uint8_t)(bs - 1)); }
-        if (rx == 16) { h.push_back((uint8_t)(rv >> 8)); h.push_back((uint8_t)rv); }
-        h.push_back(crc8(h.data(), h.size()));
         BitWriter bw;
-        bw.buf = h;
+        bw.buf = frame_header(c, f, bs, chan_code, sample_no);
         for (int ch = 0; ch < C; ch++) {
-            enc.fault = (ch == 0 && (int)f == c.fault_frame && c.fault_kind != 4) ? c.fault_kind : 0;
+            enc.fault = (ch == 0 && (int)f == c.fault_frame && c.fault_kind != 4 && c.fault_kind != 6) ? c.fault_kind : 0;
+            enc.force_verbatim = plant && ch == 0;
             enc.write_subframe(bw, sub[ch], ubps[ch], side[ch], bs);
             enc.fault = 0;
+            enc.force_verbatim = false;
         }
         bw.align();
         uint16_t crc = crc16(bw.buf.data(), bw.buf.size());
@@ -645,6 +722,18 @@ int flacgen_generate(const flacgen_config* cfg, flacgen_output* out) {
     out->frame_offsets = (uint64_t*)std::malloc(std::max<size_t>(1, frame_offs.size() * sizeof(uint64_t)));
     for (size_t i = 0; i < frame_offs.size(); i++) out->frame_offsets[i] = frame_offs[i] + out->frames_begin;
     return 0;
+}
+
+int flacgen_generate(const flacgen_config* cfg, flacgen_output* out) { return generate_impl(cfg, nullptr, out); }
+
+int flacgen_generate_pcm(const flacgen_config* cfg, const int32_t* pcm, uint64_t len, flacgen_output* out) {
+    if (!pcm || cfg->channels < 1 || len % (uint64_t)cfg->channels) return -1;
+    flacgen_config c = *cfg;
+    c.n_samples = len / (uint64_t)cfg->channels;
+    const int64_t lo = -(int64_t(1) << (c.bps - 1)), hi = (int64_t(1) << (c.bps - 1)) - 1;
+    for (uint64_t i = 0; i < len; i++)
+        if (pcm[i] < lo || pcm[i] > hi) return -1;
+    return generate_impl(&c, pcm, out);
 }
 
 void flacgen_free(flacgen_output* out) {

@@ -44,9 +44,22 @@ typedef struct flacgen_config {
     double stereo_corr;    /* R = corr * L + noise */
     int fault_frame;       /* frame index to corrupt, -1 = none */
     int fault_kind;        /* 1 reserved subframe type, 2 residual method 2, 3 LPC precision code 15,
-                              4 that frame has block size 1, 5 partition order not dividing the block */
+                              4 that frame has block size 1, 5 partition order not dividing the block,
+                              6 channel-0 subframe pinned to the SampleType maximum (stereo: the
+                              decorrelated output overflows), 7 LPC with the largest coefficients of
+                              the precision (decodable when the signal is quiet), 8 same but written
+                              even when zflac's InterType sums overflow */
     uint64_t n_samples;    /* per channel */
     uint64_t seed;
+    /* --- parity-edge options (all 0 = off) --- */
+    int dual_mono_every;   /* every Nth frame (f % N == N - 1) R = L - dual_mono_offset: constant side */
+    int dual_mono_offset;
+    int const_side;        /* constant side subframes: 0 never (coded as fixed/verbatim), 1 zflac width
+                              (bits_per_sample - wasted, src/zflac.zig:447), 2 RFC width (bps + 1 - wasted) */
+    int plant_sync_every;  /* every Nth frame (f % N == N - 1), channel 0 is verbatim and carries a copy
+                              of the frame's own CRC-8-valid header inside its sample data (bps 8 / 16 /
+                              24, independent channels only) */
+    int allow_side_overflow; /* 1 = write side channels that do not fit the SampleType (out of domain) */
 } flacgen_config;
 
 typedef struct flacgen_output {
@@ -64,6 +77,9 @@ void flacgen_default_config(flacgen_config *c);
 /* Returns 0 on success, a negative code if the requested configuration cannot be
  * written inside the parity domain (e.g. side channel overflow). */
 int flacgen_generate(const flacgen_config *c, flacgen_output *out);
+/* Same, but encodes the given interleaved PCM (n_samples = len / channels per channel,
+ * unjustified values within bps) instead of the synthetic signal. */
+int flacgen_generate_pcm(const flacgen_config *c, const int32_t *pcm, uint64_t len, flacgen_output *out);
 void flacgen_free(flacgen_output *out);
 
 #ifdef __cplusplus

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import synth
 
+from . import edges
 from .util import patch, streaminfo_offset
 
 BASE = dict(channels=2, bps=16, block_size=4096, order=8, stereo_mode=10, n_samples=4096 * 5, seed=77)
@@ -67,9 +68,13 @@ def cases():
     out["metadata_type_127"] = (bytes(b) + bytes([0xFF, 0, 0, 0]) + st.flac[st.frames_begin:], "InvalidMetadataHeader")
     # STREAMINFO relabelled as PADDING -> no STREAMINFO (:309)
     out["missing_streaminfo"] = (patch(st.flac, 4, (st.flac[4] & 0x80) | 1), "MissingStreaminfo")
-    # wrong metadata length: STREAMINFO still read as 34 bytes (:228-240), so the frame
-    # section starts 6 bytes "early" from the reference's point of view: faulty/11
-    out["incorrect_metadata_length"] = (patch(st.flac, 7, 40), None)
+    # a STREAMINFO length field of 40: zflac reads STREAMINFO as a fixed 34 bytes whatever
+    # the field says (:228-240), so the stream decodes. (faulty/11 proper, a skipped block
+    # whose length is wrong -> InvalidMetadataHeader, is tests/edges.py's
+    # incorrect_metadata_length_case.)
+    out["streaminfo_length_40"] = (patch(st.flac, 7, 40), "OK")
+    out["incorrect_metadata_length"] = (edges.incorrect_metadata_length_case(st.flac, st.frames_begin),
+                                        "InvalidMetadataHeader")  # tests/std_faulty.zig:59-61
     md5o = streaminfo_offset(st.flac) + 18
     out["wrong_md5"] = (patch(st.flac, md5o, st.flac[md5o] ^ 0x5A), "InvalidChecksum")  # :279-280
     out["wrong_channel_count"] = (_set_si_field(st.flac, _si_channels(1)), "InconsistentParameters")  # :386

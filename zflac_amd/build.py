@@ -23,6 +23,12 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in DEPS)
 
 
+def _obj_deps(src: str):
+    """Headers a translation unit includes (decode.inc only for the decode units)."""
+    hdrs = [h for h in HEADERS if not h.endswith("decode.inc") or "decode_k" in src]
+    return [src] + hdrs + [os.path.join(ROOT, "include", "zflac_hip.h")]
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB
@@ -30,8 +36,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
     build_dir = os.path.join(HERE, "_build")
     os.makedirs(build_dir, exist_ok=True)
     procs = []
-    for src in SOURCES:  # translation units compile in parallel
+    for src in SOURCES:  # translation units compile in parallel; up-to-date objects are kept
         obj = os.path.join(build_dir, os.path.basename(src) + ".o")
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d)
+                                                                               for d in _obj_deps(src)):
+            objs.append(obj)
+            continue
         cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-Wall",
                "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
         if src.endswith(".hip"):

@@ -299,6 +299,7 @@ struct zflac_batch {
     std::vector<std::unique_ptr<zflac::Class>> classes;
     hipEvent_t ev[8] = {};
     bool have_timing = false;
+    bool ran = false;  // results exist only after a completed batch_run
     zflac::DevBuf<zflac::Md5Job> md5_jobs;
     zflac::DevBuf<uint32_t> md5_dig;
     zflac_timings timings = {};
@@ -371,6 +372,11 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
         std::memset(&D, 0, sizeof(D));
         D.in_begin = in_off[m] + s.frames_begin;
         D.in_end = in_off[m] + s.len;
+        // each stream's region starts on a 32-byte boundary, whatever the length of the
+        // streams before it: the packed 16-byte stores of the fast path need 16-byte aligned
+        // frames, and zflac's backing is 32-byte aligned (:331)
+        const uint64_t align_elems = 32 / (uint64_t)esz;
+        out = (out + align_elems - 1) & ~(align_elems - 1);
         D.out_base = out;
         D.valid_total = s.si.total > 0;
         D.total = D.valid_total ? s.si.total * (uint64_t)s.nch : 0;
@@ -398,7 +404,7 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
         est_frames += (s.si.total ? s.si.total / minb : (s.len / 16)) + 2;
     }
     C.out_elems = out;
-    C.out.alloc(out * esz + 16);
+    C.out.alloc(out * esz + 32);
     ck(hipMemcpy(C.in.p, staging.data(), staging.size(), hipMemcpyHostToDevice));
     C.d_desc.alloc(C.desc.size());
     ck(hipMemcpy(C.d_desc.p, C.desc.data(), C.desc.size() * sizeof(StreamDesc), hipMemcpyHostToDevice));
@@ -984,8 +990,10 @@ int zflac_hip_batch_create(const zflac_stream* streams, size_t n, int device, in
 
 int zflac_hip_batch_run(zflac_batch* b) {
     if (!b) return E_INVALID_ARGUMENT;
+    b->ran = false;
     try {
         run_batch(b);
+        b->ran = true;
     } catch (const DeviceError&) {
         return E_DEVICE;
     } catch (const std::bad_alloc&) {
@@ -997,19 +1005,19 @@ int zflac_hip_batch_run(zflac_batch* b) {
 size_t zflac_hip_batch_size(zflac_batch* b) { return b ? b->streams.size() : 0; }
 
 int zflac_hip_batch_info(zflac_batch* b, size_t i, zflac_info* info) {
-    if (!b || i >= b->streams.size()) return E_INVALID_ARGUMENT;
+    if (!b || !b->ran || i >= b->streams.size()) return E_INVALID_ARGUMENT;
     const StreamState& s = b->streams[i];
     if (info) *info = s.info;
     return s.err;
 }
 
 const void* zflac_hip_batch_device_samples(zflac_batch* b, size_t i) {
-    if (!b || i >= b->streams.size() || b->streams[i].err) return nullptr;
+    if (!b || !b->ran || i >= b->streams.size() || b->streams[i].err) return nullptr;
     return b->streams[i].dev_samples;
 }
 
 int zflac_hip_batch_read(zflac_batch* b, size_t i, void* out, size_t out_bytes, int verify_md5) {
-    if (!b || i >= b->streams.size()) return E_INVALID_ARGUMENT;
+    if (!b || !b->ran || i >= b->streams.size()) return E_INVALID_ARGUMENT;
     StreamState& s = b->streams[i];
     if (s.err) return s.err;
     if (out_bytes < s.info.samples_bytes || (!out && s.info.samples_bytes)) return E_INVALID_ARGUMENT;
@@ -1026,7 +1034,7 @@ int zflac_hip_batch_read(zflac_batch* b, size_t i, void* out, size_t out_bytes, 
 }
 
 int zflac_hip_batch_md5(zflac_batch* b, size_t i, uint8_t* digest) {
-    if (!b || i >= b->streams.size() || !digest) return E_INVALID_ARGUMENT;
+    if (!b || !b->ran || i >= b->streams.size() || !digest) return E_INVALID_ARGUMENT;
     const StreamState& s = b->streams[i];
     if (!s.md5_dev) return E_INVALID_ARGUMENT;
     std::memcpy(digest, s.md5_dig, 16);
