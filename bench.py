@@ -1,4 +1,5 @@
-"""Benchmark: device-resident FLAC decode of the C5 per-GPU shard.
+"""Benchmark: device-resident FLAC decode of the C5 per-GPU shard, plus the drop-in
+decode() measured end to end.
 
 Workload (BASELINE.json configs[4], per-GPU share; its codec parameters are configs[2]):
 1250 independent stereo 16-bit mid/side streams per GPU, 32 frames x 4096 samples each,
@@ -9,13 +10,26 @@ inputs already in HBM, outputs left in HBM. N GPUs = N ranks with disjoint shard
 scaling, no collective in the data path; torch.distributed only for the timing barrier
 and the max over ranks).
 
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment launches the N
+ranks itself (one child process per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set
+before any HIP call); under torchrun WORLD_SIZE must equal --gpus. `--dry-run` runs the
+launcher, sharding and aggregation on CPU over gloo without touching a GPU (tests).
+
+Beside the headline (rank 0, N = 1 only): the device MD5 leg (k_md5), the CPU oracle on
+the host's cores (decode alone, and decode + MD5 as zflac's decode() does, all cores and
+one thread) and the drop-in decode() end to end (host bytes -> samples in host memory,
+STREAMINFO MD5 verified) on long single streams, with its breakdown.
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -29,13 +43,15 @@ STREAMS_PER_GPU = 1250
 FRAMES_PER_STREAM = 32
 BLOCK = 4096
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak
+METRIC = "Msamples/s decoded (bit-exact) + achieved HBM GB/s, 4096-blk stereo"
 # PMC summary of the current k_decode build (tools/pmc.sh + tools/pmc_summary.py; FETCH_SIZE /
 # WRITE_SIZE corrected by the factors tools/calib_pmc.hip measures for this access pattern)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_current.json")
 
 
-def pmc_traffic(kernel: str):
-    """Corrected HBM bytes per launch of `kernel` from the committed PMC summary, or None."""
+def pmc_traffic(kernel: str, lib_sha: str | None):
+    """Corrected HBM bytes per launch of `kernel` from the committed PMC summary, or None;
+    only when the summary was taken on the library build being timed (same sha256)."""
     try:
         with open(PMC_SUMMARY) as f:
             d = json.load(f)
@@ -44,23 +60,50 @@ def pmc_traffic(kernel: str):
     row = d.get("kernels", {}).get(kernel)
     if not row or "hbm_traffic_bytes" not in row:
         return None
-    return {"bytes": int(row["hbm_traffic_bytes"]), "read": int(row["hbm_read_bytes"]),
-            "write": int(row["hbm_write_bytes"]), "source": os.path.relpath(d.get("_source", PMC_SUMMARY), ROOT)}
+    same = lib_sha is not None and d.get("lib_sha256") == lib_sha
+    return {"bytes": int(row["hbm_traffic_bytes"]) if same else None, "read": int(row["hbm_read_bytes"]),
+            "write": int(row["hbm_write_bytes"]), "same_build": same, "lib_sha256": d.get("lib_sha256"),
+            "source": os.path.relpath(d.get("_source", PMC_SUMMARY), ROOT)}
 
 
 def parse_args():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (one per GPU); default WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--streams-per-gpu", type=int, default=STREAMS_PER_GPU)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample budget (all cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-md5", action="store_true", help="skip the device-MD5 leg")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the single-stream decode() legs")
+    ap.add_argument("--e2e-frames", type=int, default=65536, help="frames of the long single stream")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default=None)
+    ap.add_argument("--same-device", action="store_true", help="every rank on GPU 0 (multi-process test)")
+    ap.add_argument("--dry-run", action="store_true", help="CPU only: launcher, shards, aggregation")
     return ap.parse_args()
 
 
+# ------------------------------------------------------------------------ launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(n: int) -> int:
+    """Spawn n ranks of this script (the parent never touches a GPU) and wait for them."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc), 0)
+
+
+# ------------------------------------------------------------------------ workload
 def make_shard(rank: int, world: int, n_streams: int):
     import synth
     from zflac_amd.shard import shard_range
@@ -71,8 +114,7 @@ def make_shard(rank: int, world: int, n_streams: int):
 
     def work(k):
         for i in range(k, n_streams, workers):
-            st = synth.generate(**cfgs[i])
-            out[i] = st.flac  # keep only the compressed bytes; MD5 lives in STREAMINFO
+            out[i] = synth.generate(**cfgs[i]).flac  # MD5 lives in STREAMINFO
     ts = [threading.Thread(target=work, args=(k,)) for k in range(workers)]
     for t in ts:
         t.start()
@@ -81,22 +123,32 @@ def make_shard(rank: int, world: int, n_streams: int):
     return out
 
 
-def cpu_baseline(streams, seconds: float):
-    """The oracle (C restatement of zflac decode, ReleaseFast-like build) on host cores,
-    independent streams in parallel; bounded sample."""
+def host_cores() -> tuple[int, str]:
+    """CPUs this job may use: the affinity set, capped by a cgroup CPU quota if any."""
+    n = len(os.sched_getaffinity(0))
+    note = f"sched_getaffinity {n}"
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(p)))
+            note += f", cgroup quota {quota}"
+            n = min(n, quota)
+    except (OSError, ValueError):
+        pass
+    return n, note
+
+
+def _oracle_rate(streams, seconds: float, threads: int, md5: bool):
     import oracle
 
-    oracle.decode_count_only(streams[0])  # load
-    threads = min(16, os.cpu_count() or 1)
     counts = [0] * threads
     stop = time.perf_counter() + seconds
     t0 = time.perf_counter()
 
     def work(k):
-        i = k
-        n = 0
+        i, n = k, 0
         while time.perf_counter() < stop:
-            err, ns = oracle.decode_count_only(streams[i % len(streams)])
+            err, ns = oracle.decode_count_only(streams[i % len(streams)], "fast", md5=md5)
             assert err == 0
             n += ns
             i += threads
@@ -107,10 +159,28 @@ def cpu_baseline(streams, seconds: float):
     for t in ts:
         t.join()
     dt = time.perf_counter() - t0
-    total = sum(counts)
-    return {"value": total / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/zflac_oracle.c (-O3 -march=x86-64-v4, Debug checks off) decoding C5 shard streams "
-                      f"round-robin on {threads} threads for {dt:.1f} s ({total / 1e6:.0f} M samples, MD5 incl.)"}
+    return sum(counts) / dt / 1e6, sum(counts), dt
+
+
+def cpu_baseline(streams, seconds: float):
+    """The oracle (C restatement of zflac decode, ReleaseFast-like build) on the host:
+    bounded samples of the shard's streams. `value` is the decode alone on every core
+    (like-for-like with the device headline, which excludes MD5); decode + MD5 (what
+    zflac's decode() does) on every core and on one thread are reported beside it."""
+    import oracle
+
+    oracle.decode_count_only(streams[0])  # load
+    cores, note = host_cores()
+    v_dec, n_dec, t_dec = _oracle_rate(streams, seconds, cores, md5=False)
+    v_md5, _, _ = _oracle_rate(streams, seconds / 2, cores, md5=True)
+    v_1t, _, _ = _oracle_rate(streams[:1], 3.0, 1, md5=True)
+    v_1t_dec, _, _ = _oracle_rate(streams[:1], 2.0, 1, md5=False)
+    return {"value": round(v_dec, 1), "unit": "Msamples/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/zflac_oracle.c (-O3 -march=x86-64-v4, Debug checks off), decode only (MD5 "
+                      f"skipped), C5 shard streams round-robin on {cores} threads ({note}) for {t_dec:.1f} s "
+                      f"({n_dec / 1e6:.0f} M samples)",
+            "value_with_md5": round(v_md5, 1), "value_1thread_with_md5": round(v_1t, 1),
+            "value_1thread": round(v_1t_dec, 1)}
 
 
 def verify(batch, streams, n_check_oracle=4):
@@ -141,42 +211,122 @@ def verify(batch, streams, n_check_oracle=4):
     return errs
 
 
+def e2e_leg(name: str, cfg: dict, seg_frames: int, frames: int, oracle_full: bool):
+    """decode() end to end on one stream: zflac_hip_open (plan, H2D, device decode) +
+    zflac_hip_read (D2H overlapped with the host STREAMINFO MD5), best of 2, with the
+    oracle's one-thread decode() of the same stream beside it."""
+    import oracle
+    import synth
+    import zflac_amd
+
+    st = synth.generate(**dict(cfg, n_samples=BLOCK * seg_frames))
+    reps = max(1, frames // seg_frames)
+    data = synth.tile_flac(st, reps) if reps > 1 else st.flac
+    n = st.pcm.size * reps
+    best = None
+    for _ in range(2):
+        tm = {}
+        t0 = time.perf_counter()
+        d = zflac_amd.decode(data, timings=tm)  # raises InvalidChecksum unless bit-exact
+        wall = time.perf_counter() - t0
+        assert d.samples.values.size == n
+        if best is None or wall < best[0]:
+            best = (wall, tm)
+        del d
+    wall, tm = best
+    if oracle_full:
+        t0 = time.perf_counter()
+        err, ns = oracle.decode_count_only(data, "fast")
+        cpu_s = time.perf_counter() - t0
+        cpu_note = "whole stream"
+    else:  # bounded: the repeated segment, scaled (same frames, same work per frame)
+        t0 = time.perf_counter()
+        err, ns = oracle.decode_count_only(st.flac, "fast")
+        cpu_s = (time.perf_counter() - t0) * reps
+        cpu_note = f"one {seg_frames}-frame segment x {reps}"
+    assert err == 0
+    out_bytes = n * (2 if cfg["bps"] <= 16 else 4)
+    return {"stream": name, "frames": seg_frames * reps, "channel_samples": int(n), "input_bytes": len(data),
+            "output_bytes": int(out_bytes), "wall_ms": round(wall * 1e3, 1),
+            "msps": round(n / wall / 1e6, 1),
+            "breakdown_ms": {"plan": round(tm["plan_ms"], 2), "upload_h2d": round(tm["upload_ms"], 2),
+                             "device_run": round(tm["run_wall_ms"], 2), "kernels": round(tm["total_ms"], 3),
+                             "read_d2h_with_md5": round(tm["read_ms"], 2), "host_md5": round(tm["host_md5_ms"], 2)},
+            "oracle_1thread_ms": round(cpu_s * 1e3, 1), "oracle_1thread_msps": round(n / cpu_s / 1e6, 1),
+            "oracle_sample": cpu_note, "speedup_vs_oracle_1thread": round(cpu_s / wall, 2),
+            "md5_bound_msps": round(n / (tm["host_md5_ms"] * 1e-3) / 1e6, 1) if tm["host_md5_ms"] else None}
+
+
+# ------------------------------------------------------------------------ main
 def main():
     args = parse_args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus and args.gpus > 1:
+        sys.exit(launch(args.gpus))
+    world = int(env_world or 1)
+    if args.gpus is not None and args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    device = 0 if args.same_device else local_rank
+    backend = args.backend or ("gloo" if (args.dry_run or args.same_device) else "nccl")
     dist = None
     if world > 1:
         import torch
         import torch.distributed as tdist
 
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(device)
+        tdist.init_process_group(backend, rank=rank, world_size=world)
         dist = tdist
+    coll_dev = "cuda" if (dist is not None and backend == "nccl") else None
 
-    import zflac_amd
+    def barrier_sync():
+        if dist is not None:
+            dist.barrier()
+            if backend == "nccl":
+                import torch
+
+                torch.cuda.synchronize()
+
+    from zflac_amd.shard import aggregate, shard_range
 
     t_gen = time.perf_counter()
     streams = make_shard(rank, world, args.streams_per_gpu)
     t_gen = time.perf_counter() - t_gen
-    batch = zflac_amd.Batch(streams, device=local_rank, timing=True)
 
-    def barrier_sync():
+    if args.dry_run:  # no GPU: the launch / shard / aggregation path only
+        barrier_sync()
+        t0 = time.perf_counter()
+        samples = sum(int.from_bytes(s[21:26], "big") & ((1 << 36) - 1) for s in streams) * 2
+        barrier_sync()
+        el = time.perf_counter() - t0
+        tot = aggregate(dist, coll_dev, el, samples, sum(len(s) for s in streams), samples * 2, 0)
+        shards = [None] * world
+        rng = shard_range(rank, world, args.streams_per_gpu)
+        mine = [rng.start, rng.stop]
         if dist is not None:
-            import torch
+            dist.all_gather_object(shards, mine)
+        else:
+            shards = [mine]
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "value": None,
+                              "config": {"streams_total": args.streams_per_gpu * world,
+                                         "parallelism": f"stream-shard x{world}"},
+                              "shards": shards, "samples_total": tot.samples, "backend": backend,
+                              "digest_rank0": hashlib.sha256(b"".join(streams)).hexdigest()[:16]}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
-            dist.barrier()
-            torch.cuda.synchronize()
+    import zflac_amd
 
+    batch = zflac_amd.Batch(streams, device=device, timing=True)
     for _ in range(args.warmup):
         batch.run()
     barrier_sync()
     t0 = time.perf_counter()
-    dec_ms = []
-    walk_ms = []
-    scan_ms = []
-    ver_ms = []
+    dec_ms, walk_ms, scan_ms, ver_ms = [], [], [], []
     for _ in range(args.steps):
         batch.run()
         t = batch.timings()
@@ -191,9 +341,7 @@ def main():
     in_bytes, out_bytes = tm.input_bytes, tm.output_bytes
 
     errs = [] if args.no_verify else verify(batch, streams)
-    from zflac_amd.shard import aggregate
-
-    tot = aggregate(dist, "cuda" if dist is not None else None, elapsed, samples_rank, in_bytes, out_bytes, len(errs))
+    tot = aggregate(dist, coll_dev, elapsed, samples_rank, in_bytes, out_bytes, len(errs))
     elapsed = tot.elapsed_s
     samples_all, in_all, out_all = tot.samples, tot.input_bytes, tot.output_bytes
     ok = tot.errors == 0
@@ -203,7 +351,8 @@ def main():
     md5 = None
     if not args.no_md5:
         batch.close()
-        mb = zflac_amd.Batch(streams, device=local_rank, timing=True, device_md5=True)
+        batch = None
+        mb = zflac_amd.Batch(streams, device=device, timing=True, device_md5=True)
         md5_ms, tot_ms = [], []
         for k in range(3):
             mb.run()
@@ -218,11 +367,18 @@ def main():
                "hashed_bytes_rank0": int(out_bytes),
                "note": "one lane per stream (MD5 is a serial chain per stream); not in `value`"}
         ok = ok and md5_ok
-        batch = None
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(streams, args.cpu_seconds)
+    e2e = None
+    if rank == 0 and world == 1:
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(streams, args.cpu_seconds)
+        if not args.no_e2e:
+            import synth
+
+            e2e = [e2e_leg("C3 stereo M/S 16-bit LPC-8, 65536 frames (SURVEY 8d size)", synth.config_c3(),
+                           1024, args.e2e_frames, oracle_full=False),
+                   e2e_leg("C3, 2600 frames (a ~4-minute track)", synth.config_c3(), 2600, 2600, oracle_full=True)]
 
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
@@ -230,10 +386,10 @@ def main():
         dec_avg = float(np.mean(dec_ms))
         alg_bytes = in_bytes + out_bytes  # per decode launch (this rank)
         achieved = alg_bytes / (dec_avg * 1e-3) / 1e9
-        pmc = pmc_traffic("zflac::k_decode<1, 2>")
-        traffic = pmc["bytes"] if pmc else None
+        lib_sha = hashlib.sha256(open(zflac_amd.lib_path, "rb").read()).hexdigest()
+        pmc = pmc_traffic("zflac::k_decode<1, 2>", lib_sha)
         line = {
-            "metric": "Msamples/s decoded (bit-exact) + achieved HBM GB/s, 4096-blk stereo",
+            "metric": METRIC,
             "value": round(value, 1),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -252,19 +408,23 @@ def main():
             "hbm_gbs_step": round((in_all + out_all) * args.steps / elapsed / 1e9, 1),
             "bit_exact": ok,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc["bytes"] if pmc else None,
                          "kernel": "k_decode<1, 2>", "kernel_ms": round(dec_avg, 4),
                          "alg_bytes_per_launch": int(alg_bytes)},
             "stages_ms": {"scan+compact": round(float(np.mean(scan_ms)), 4),
                           "walk": round(float(np.mean(walk_ms)), 4), "decode": round(dec_avg, 4),
                           "verify": round(float(np.mean(ver_ms)), 4)},
             "traffic_detail": pmc,
+            "lib_sha256": lib_sha[:16],
             "device_md5": md5,
             "cpu_baseline": cpu,
+            "e2e_decode": e2e,
             "gen_seconds": round(t_gen, 2),
         }
         if cpu:
-            line["gpu_over_cpu"] = round(value / cpu["value"], 1)
+            line["gpu_over_cpu"] = round(value / cpu["value"], 1)  # decode alone on both sides
+            if md5:
+                line["gpu_over_cpu_with_md5"] = round(md5["decode_plus_md5_msps_rank0"] / cpu["value_with_md5"], 1)
         print(json.dumps(line), flush=True)
         if errs:
             print("BIT-EXACTNESS FAILURES:", errs[:10], file=sys.stderr)

@@ -81,6 +81,12 @@ typedef struct zflac_timings {
     uint64_t samples;       /* channel-samples written */
     double walk_ms;     /* subframe-start walk k_walk (2+ channels; runs before k_decode) */
     double md5_ms;      /* batched STREAMINFO MD5 k_md5 (ZFLAC_FLAG_DEVICE_MD5), else 0 */
+    /* host wall-clock times (steady clock), recorded whether or not ZFLAC_FLAG_TIMING is set */
+    double plan_ms;     /* batch_create / open: metadata and first-frame parse */
+    double upload_ms;   /* batch_create / open: staging + H2D of the compressed bytes, allocations */
+    double run_wall_ms; /* last batch_run, launch to results (kernels + read-backs) */
+    double read_ms;     /* last batch_read / read: D2H of the samples (+ MD5 overlapped) */
+    double host_md5_ms; /* last batch_read / read: host STREAMINFO MD5 (overlapped with the D2H) */
 } zflac_timings;
 
 typedef struct zflac_batch zflac_batch;
@@ -93,7 +99,9 @@ typedef struct zflac_batch zflac_batch;
 int zflac_hip_open(const uint8_t *buf, size_t len, int device, zflac_batch **out_batch, zflac_info *info);
 /* Copy the samples into caller memory, verify the STREAMINFO MD5
  * (ZFLAC_E_INVALID_CHECKSUM on mismatch, as src/zflac.zig:279-280), left-justify is
- * already applied on the device (src/zflac.zig:287-306). */
+ * already applied on the device (src/zflac.zig:287-306). Long streams are copied back in
+ * chunks while a host thread hashes the chunks already landed (MD5 is one serial chain per
+ * stream, so it bounds this call). */
 int zflac_hip_read(zflac_batch *b, void *out_samples, size_t out_bytes);
 void zflac_hip_close(zflac_batch *b);
 
@@ -105,7 +113,9 @@ int zflac_hip_batch_create(const zflac_stream *streams, size_t n, int device, in
  * outputs left in HBM). Synchronous. Returns ZFLAC_OK or ZFLAC_E_DEVICE; per-stream
  * zflac errors are reported by zflac_hip_batch_info. */
 int zflac_hip_batch_run(zflac_batch *b);
-/* Per-stream result of the last run: zflac error code, and shape when OK. */
+/* Per-stream result of the last run: zflac error code, and shape when OK.
+ * Before the first completed run: ZFLAC_E_INVALID_ARGUMENT (as for _read, _md5 and
+ * _device_samples, which returns NULL). */
 int zflac_hip_batch_info(zflac_batch *b, size_t i, zflac_info *info);
 /* Copy stream i's samples to host memory; verify_md5 != 0 checks STREAMINFO MD5. */
 int zflac_hip_batch_read(zflac_batch *b, size_t i, void *out, size_t out_bytes, int verify_md5);
@@ -115,6 +125,8 @@ int zflac_hip_batch_read(zflac_batch *b, size_t i, void *out, size_t out_bytes, 
 int zflac_hip_batch_md5(zflac_batch *b, size_t i, uint8_t *digest16);
 /* Device pointer of stream i's samples (valid until the next run / destroy). */
 const void *zflac_hip_batch_device_samples(zflac_batch *b, size_t i);
+/* Timings of the last run / read. ZFLAC_OK when device timings were recorded
+ * (ZFLAC_FLAG_TIMING); the host wall-clock fields are filled either way. */
 int zflac_hip_batch_timings(zflac_batch *b, zflac_timings *t);
 size_t zflac_hip_batch_size(zflac_batch *b);
 void zflac_hip_batch_destroy(zflac_batch *b);

@@ -47,6 +47,8 @@ def _lib(flavor="checked"):
         lib = ctypes.CDLL(_LIBS[flavor])
         lib.zfo_decode.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(_Result)]
         lib.zfo_decode.restype = ctypes.c_int
+        lib.zfo_decode_ex.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(_Result)]
+        lib.zfo_decode_ex.restype = ctypes.c_int
         lib.zfo_free.argtypes = [ctypes.POINTER(_Result)]
         lib.zfo_md5.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
         lib.zfo_error_name.restype = ctypes.c_char_p
@@ -80,11 +82,12 @@ def decode(data: bytes, flavor: str = "checked") -> OracleResult:
         lib.zfo_free(ctypes.byref(r))
 
 
-def decode_count_only(data: bytes, flavor: str = "fast") -> tuple[int, int]:
-    """Decode and return (err, n_samples) without copying samples (for timing)."""
+def decode_count_only(data: bytes, flavor: str = "fast", md5: bool = True) -> tuple[int, int]:
+    """Decode and return (err, n_samples) without copying samples (for timing); md5=False
+    skips the STREAMINFO MD5 (the decode alone)."""
     lib = _lib(flavor)
     r = _Result()
-    err = lib.zfo_decode(data, len(data), ctypes.byref(r))
+    err = lib.zfo_decode_ex(data, len(data), 0 if md5 else 1, ctypes.byref(r))
     n = r.n_samples
     lib.zfo_free(ctypes.byref(r))
     return err, n

@@ -631,7 +631,9 @@ fail:
 }
 
 /* decode (src/zflac.zig:217-310) */
-int zfo_decode(const uint8_t *buf, size_t len, zfo_result *res) {
+int zfo_decode(const uint8_t *buf, size_t len, zfo_result *res) { return zfo_decode_ex(buf, len, 0, res); }
+
+int zfo_decode_ex(const uint8_t *buf, size_t len, int flags, zfo_result *res) {
     memset(res, 0, sizeof(*res));
     rd r = {buf, len, 0, (uint64_t)len * 8};
     uint64_t sig;
@@ -697,19 +699,23 @@ int zfo_decode(const uint8_t *buf, size_t len, zfo_result *res) {
     else memcpy(out, s32, n * 4);
     free(s32);
 
-    /* MD5 over the output bytes; 24-bit containers hash 3 bytes per sample (:267-280) */
-    uint8_t md5[16];
-    md5_ctx c;
-    md5_init(&c);
-    if (aligned == 24) {
-        for (uint64_t i = 0; i < n; i++) md5_update(&c, out + 4 * i, 3);
-    } else {
-        md5_update(&c, out, n * esz);
+    /* MD5 over the output bytes; 24-bit containers hash 3 bytes per sample (:267-280).
+     * ZFO_NO_MD5 skips it (timing of the decode alone; not zflac's behaviour). */
+    int md5_bad = 0;
+    if (!(flags & ZFO_NO_MD5)) {
+        uint8_t md5[16];
+        md5_ctx c;
+        md5_init(&c);
+        if (aligned == 24) {
+            for (uint64_t i = 0; i < n; i++) md5_update(&c, out + 4 * i, 3);
+        } else {
+            md5_update(&c, out, n * esz);
+        }
+        md5_final(&c, md5);
+        /* decode() fails with InvalidChecksum (:279-280); the samples are still handed back
+         * (justified) so tests can compare what both decoders produced for such a stream */
+        md5_bad = memcmp(md5, si.md5, 16) != 0;
     }
-    md5_final(&c, md5);
-    /* decode() fails with InvalidChecksum (:279-280); the samples are still handed back
-     * (justified) so tests can compare what both decoders produced for such a stream */
-    const int md5_bad = memcmp(md5, si.md5, 16) != 0;
 
     /* left-justify AFTER the MD5 (:287-306) */
     if (depth >= 9 && depth <= 15) {

@@ -59,6 +59,10 @@ typedef struct zfo_result {
 /* Full decode() semantics: signature, metadata walk, frames, MD5 verification,
  * left-justify (src/zflac.zig:217-310). */
 int zfo_decode(const uint8_t *buf, size_t len, zfo_result *out);
+/* zfo_decode with options: ZFO_NO_MD5 skips the STREAMINFO MD5 (CPU timing of the decode
+ * alone, beside the device decode that `bench.py`'s headline excludes MD5 from). */
+#define ZFO_NO_MD5 1
+int zfo_decode_ex(const uint8_t *buf, size_t len, int flags, zfo_result *out);
 void zfo_free(zfo_result *r);
 const char *zfo_error_name(int code);
 

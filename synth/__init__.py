@@ -152,3 +152,44 @@ def config_c4(n_frames=64, seed=0x5EED0004):
 def config_c5(stream_index: int, n_frames=32):
     """C5: one of 10k independent stereo 16-bit mid/side LPC-8 streams (block 4096)."""
     return config_c3(n_frames=n_frames, seed=0x5EED0005_00000000 + stream_index)
+
+
+def md5_message(pcm: np.ndarray, bps: int) -> bytes:
+    """The bytes zflac's decode() hashes for `pcm` (src/zflac.zig:267-277): the container
+    values before left-justify, little-endian; 17..24-bit containers hash 3 bytes each."""
+    a = (bps + 7) // 8
+    if a == 1:
+        return pcm.astype(np.int8).tobytes()
+    if a == 2:
+        return pcm.astype("<i2").tobytes()
+    b = pcm.astype("<i4").view(np.uint8).reshape(-1, 4)
+    return np.ascontiguousarray(b[:, :3] if a == 3 else b).tobytes()
+
+
+def tile_flac(st: Stream, reps: int) -> bytes:
+    """`st` with its frame section repeated `reps` times: a long stream for throughput
+    runs without generating every frame (LPC analysis is the slow part of the writer).
+    STREAMINFO's total samples and MD5 are rewritten for the repeated PCM, so decode()
+    verifies the whole output. Frame numbers repeat: zflac never checks them (the coded
+    number is only parsed, src/zflac.zig:354) and each header keeps its valid CRC-8.
+    Fixed-blocksize streams with STREAMINFO first (the writer's layout) only."""
+    import hashlib
+
+    cfg = st.config
+    if cfg.get("variable_blocking"):
+        raise ValueError("tile_flac: fixed-blocksize streams only")
+    d = bytearray(st.flac[: st.frames_begin])
+    assert d[:4] == b"fLaC" and (d[4] & 0x7F) == 0
+    o = 8
+    total = int(st.pcm.size // cfg["channels"]) * reps
+    if total >= 1 << 36:
+        raise ValueError("tile_flac: total samples exceed STREAMINFO's 36 bits")
+    d[o + 13] = (d[o + 13] & 0xF0) | ((total >> 32) & 15)
+    for i in range(4):
+        d[o + 14 + i] = (total >> (8 * (3 - i))) & 0xFF
+    msg = md5_message(st.pcm, cfg["bps"])
+    h = hashlib.md5()
+    for _ in range(reps):
+        h.update(msg)
+    d[o + 18:o + 34] = h.digest()
+    return bytes(d) + st.flac[st.frames_begin:] * reps

@@ -105,3 +105,50 @@ def test_gloo_world2_shards_and_aggregates():
     for g in range(WORLD * PER_RANK):
         total += synth.generate(**_cfg(g)).pcm.size
     assert res[0][1].samples == total
+
+
+def _bench(*extra, timeout=300):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *extra], capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # ONE JSON line, from rank 0
+    return json.loads(lines[0])
+
+
+def test_bench_self_launch_dry_run():
+    """`bench.py --gpus 2` launches its two ranks itself (no torchrun): disjoint shards,
+    job totals over both ranks, one JSON line. CPU only (gloo, no HIP call)."""
+    d = _bench("--gpus", "2", "--dry-run", "--streams-per-gpu", "3", "--steps", "1", "--warmup", "0")
+    assert d["dry_run"] and d["n_gpus"] == 2 and d["backend"] == "gloo"
+    assert d["config"]["streams_total"] == 6
+    assert d["shards"] == [[0, 3], [3, 6]]
+    assert d["samples_total"] == 6 * 32 * 4096 * 2
+
+
+def test_bench_world_mismatch_fails():
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=root)
+    assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_two_hip_contexts(gpu_ready):
+    """Two ranks launched by bench.py itself, each with its own HIP context on GPU 0 (the
+    only GPU of the test box), gloo for the barrier: shards decode bit-exactly and the
+    job line covers both ranks."""
+    d = _bench("--gpus", "2", "--same-device", "--streams-per-gpu", "16", "--steps", "2", "--warmup", "1",
+               "--no-cpu-baseline", "--no-md5", "--no-e2e")
+    assert d["n_gpus"] == 2 and d["bit_exact"] is True
+    assert d["config"]["streams_total"] == 32 and d["value"] > 0

@@ -27,7 +27,9 @@ class zflac_stream(ctypes.Structure):
 class zflac_timings(ctypes.Structure):
     _fields_ = [("scan_ms", ctypes.c_double), ("decode_ms", ctypes.c_double), ("verify_ms", ctypes.c_double),
                 ("total_ms", ctypes.c_double), ("frames", ctypes.c_uint64), ("input_bytes", ctypes.c_uint64),
-                ("output_bytes", ctypes.c_uint64), ("samples", ctypes.c_uint64), ("walk_ms", ctypes.c_double), ("md5_ms", ctypes.c_double)]
+                ("output_bytes", ctypes.c_uint64), ("samples", ctypes.c_uint64), ("walk_ms", ctypes.c_double),
+                ("md5_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("upload_ms", ctypes.c_double),
+                ("run_wall_ms", ctypes.c_double), ("read_ms", ctypes.c_double), ("host_md5_ms", ctypes.c_double)]
 
 
 # every symbol include/zflac_hip.h declares, with (restype, argtypes)

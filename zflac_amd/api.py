@@ -73,8 +73,9 @@ def _aligned_empty(nbytes: int, dtype) -> np.ndarray:
     return raw[off:off + nbytes].view(dtype)
 
 
-def decode(reader, device: int = 0) -> DecodedFLAC:
-    """Decode one FLAC stream on `device`; raises zflac-named errors (errors.*)."""
+def decode(reader, device: int = 0, timings: dict | None = None) -> DecodedFLAC:
+    """Decode one FLAC stream on `device`; raises zflac-named errors (errors.*).
+    `timings` (a dict) receives the library's host wall-clock breakdown of the call."""
     data = _read_all(reader)
     L = _lib.load()
     handle = ctypes.c_void_p()
@@ -86,6 +87,10 @@ def decode(reader, device: int = 0) -> DecodedFLAC:
         rc = L.zflac_hip_read(handle, out.ctypes.data_as(ctypes.c_void_p) if info.samples_bytes else None,
                               info.samples_bytes)
         errors.check(rc)
+        if timings is not None:
+            t = _lib.zflac_timings()
+            L.zflac_hip_batch_timings(handle, ctypes.byref(t))
+            timings.update({name: getattr(t, name) for name, _ in _lib.zflac_timings._fields_})
         return DecodedFLAC(info.channels, info.sample_rate, info.bits_per_sample,
                            Samples(_TAGS[info.sample_kind], out))
     finally:

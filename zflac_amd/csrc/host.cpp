@@ -7,6 +7,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -67,6 +69,10 @@ hipError_t launch_verify(const VerifyArgs& a, uint32_t max_items, hipStream_t st
 hipError_t launch_md5(const Md5Job* jobs, uint32_t n_jobs, uint32_t* digests, hipStream_t st);
 
 namespace {
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 struct DeviceError {};
 inline void ck(hipError_t e) {
@@ -348,6 +354,71 @@ void plan_stream(StreamState& s, const uint8_t* d, size_t n) {
     if (channels_count_h(s.first.chan_code) != s.nch) { s.host_err = E_INCONSISTENT_PARAMETERS; return; }  // :386
 }
 
+// Copy streams into their HBM layout (stream m at in_off[m], zeros elsewhere, `total`
+// bytes) through two pinned 32 MiB windows: host threads fill one window while the DMA
+// engine drains the other. The windows are a lazily created per-process context, shared
+// by all batches under a lock.
+struct Uploader {
+    static constexpr uint64_t WIN = 32ull << 20;
+    std::mutex mu;
+    uint8_t* pin[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    bool used[2] = {false, false};
+};
+
+Uploader& uploader() {
+    static Uploader* u = new Uploader();  // never destroyed: outlives every batch
+    return *u;
+}
+
+// bytes [a, b) of the layout into dst
+void fill_window(uint8_t* dst, uint64_t a, uint64_t b, const std::vector<uint64_t>& in_off,
+                 const std::vector<const uint8_t*>& srcs, const std::vector<uint64_t>& lens) {
+    size_t m = std::upper_bound(in_off.begin(), in_off.end(), a) - in_off.begin();
+    m = m ? m - 1 : 0;
+    uint64_t p = a;
+    for (; p < b && m < in_off.size(); m++) {
+        const uint64_t s0 = in_off[m], s1 = in_off[m] + lens[m];
+        if (s1 <= p) continue;
+        if (s0 >= b) break;
+        if (s0 > p) {
+            std::memset(dst + (p - a), 0, s0 - p);
+            p = s0;
+        }
+        const uint64_t e = std::min(s1, b);
+        std::memcpy(dst + (p - a), srcs[m] + (p - s0), e - p);
+        p = e;
+    }
+    if (p < b) std::memset(dst + (p - a), 0, b - p);
+}
+
+void upload_streams(uint8_t* dev, uint64_t total, const std::vector<uint64_t>& in_off,
+                    const std::vector<const uint8_t*>& srcs, const std::vector<uint64_t>& lens, hipStream_t st) {
+    Uploader& U = uploader();
+    std::lock_guard<std::mutex> lock(U.mu);
+    for (int k = 0; k < 2; k++) {
+        if (!U.pin[k]) ck(hipHostMalloc(reinterpret_cast<void**>(&U.pin[k]), Uploader::WIN, hipHostMallocDefault));
+        if (!U.done[k]) ck(hipEventCreate(&U.done[k]));
+    }
+    int k = 0;
+    for (uint64_t a = 0; a < total; a += Uploader::WIN, k ^= 1) {
+        const uint64_t b = std::min(a + Uploader::WIN, total);
+        if (U.used[k]) ck(hipEventSynchronize(U.done[k]));  // the DMA of this window's last use
+        const uint64_t n = b - a;
+        const int nt = n >= (8ull << 20) ? 4 : 1;
+        std::vector<std::thread> ts;
+        for (int t = 1; t < nt; t++)
+            ts.emplace_back(fill_window, U.pin[k] + n * t / nt, a + n * t / nt, a + n * (t + 1) / nt,
+                            std::cref(in_off), std::cref(srcs), std::cref(lens));
+        fill_window(U.pin[k], a, a + n / nt, in_off, srcs, lens);
+        for (auto& t : ts) t.join();
+        ck(hipMemcpyAsync(dev + a, U.pin[k], n, hipMemcpyHostToDevice, st));
+        ck(hipEventRecord(U.done[k], st));
+        U.used[k] = true;
+    }
+    ck(hipStreamSynchronize(st));
+}
+
 void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     const int esz = esz_of_kind(C.kind);
     // input layout: each stream 16-byte aligned
@@ -359,7 +430,6 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     }
     C.in_bytes = off;
     C.in.alloc(off + INPUT_PAD);
-    std::vector<uint8_t> staging(off + INPUT_PAD, 0);
     uint64_t out = 0;
     uint64_t est_frames = 0;
     C.desc.resize(C.members.size());
@@ -367,7 +437,6 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     for (size_t m = 0; m < C.members.size(); m++) {
         StreamState& s = b->streams[C.members[m]];
         s.slot = (uint32_t)m;
-        std::memcpy(staging.data() + in_off[m], src[C.members[m]].data, s.len);
         StreamDesc& D = C.desc[m];
         std::memset(&D, 0, sizeof(D));
         D.in_begin = in_off[m] + s.frames_begin;
@@ -401,11 +470,18 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
         }
         D.end_chunk = (uint32_t)C.chunks.size();
         const uint64_t minb = std::max<uint64_t>(16, s.si.min_block ? s.si.min_block : 16);
-        est_frames += (s.si.total ? s.si.total / minb : (s.len / 16)) + 2;
+        // (at most one candidate per two bytes: a huge STREAMINFO total cannot inflate it)
+        est_frames += std::min<uint64_t>(s.si.total ? s.si.total / minb : s.len / 16, s.len / 2) + 2;
     }
     C.out_elems = out;
     C.out.alloc(out * esz + 32);
-    ck(hipMemcpy(C.in.p, staging.data(), staging.size(), hipMemcpyHostToDevice));
+    std::vector<const uint8_t*> srcs(C.members.size());
+    std::vector<uint64_t> lens(C.members.size());
+    for (size_t m = 0; m < C.members.size(); m++) {
+        srcs[m] = src[C.members[m]].data;
+        lens[m] = b->streams[C.members[m]].len;
+    }
+    upload_streams(C.in.p, C.in.n, in_off, srcs, lens, b->stream);  // inputs resident in HBM
     C.d_desc.alloc(C.desc.size());
     ck(hipMemcpy(C.d_desc.p, C.desc.data(), C.desc.size() * sizeof(StreamDesc), hipMemcpyHostToDevice));
     const size_t nc = std::max<size_t>(C.chunks.size(), 1);
@@ -787,47 +863,104 @@ void run_batch(zflac_batch* b) {
 }
 
 // MD5 of the decoded stream exactly as zflac hashes it: before left-justify, 24-bit
-// containers hash 3 bytes per sample (src/zflac.zig:267-280).
-bool md5_matches(const StreamState& s, const void* host_samples) {
-    Md5 md;
-    const uint64_t n = s.info.n_samples;
-    const uint32_t bps = s.si.bps;
-    const uint8_t js = justify_of(bps);
-    if (s.kind == 0) {
-        md.update(host_samples, n);
-    } else if (s.kind == 1) {
-        if (!js) {
-            md.update(host_samples, n * 2);
-        } else {
-            const int16_t* v = static_cast<const int16_t*>(host_samples);
-            std::vector<int16_t> tmp(4096);
-            for (uint64_t i = 0; i < n; i += tmp.size()) {
-                const uint64_t m = std::min<uint64_t>(tmp.size(), n - i);
-                for (uint64_t k = 0; k < m; k++) tmp[k] = (int16_t)(v[i + k] >> js);
-                md.update(tmp.data(), m * 2);
-            }
+// containers hash 3 bytes per sample (src/zflac.zig:267-280). Fed in element-aligned
+// pieces, so the read can hash chunks as they land.
+class SampleHasher {
+public:
+    explicit SampleHasher(const StreamState& s)
+        : kind_(s.kind), js_(justify_of(s.si.bps)), w24_((s.si.bps + 7) / 8 * 8 == 24) {}
+    void update(const void* samples, uint64_t n) {  // n elements of the stream's container
+        if (kind_ == 0 || (kind_ == 1 && !js_) || (kind_ == 2 && !js_ && !w24_)) {
+            md_.update(samples, n * (kind_ == 0 ? 1 : kind_ == 1 ? 2 : 4));
+            return;
         }
-    } else {
-        const int32_t* v = static_cast<const int32_t*>(host_samples);
-        const uint32_t aligned = (bps + 7) / 8 * 8;
-        if (aligned == 32 && !js) {
-            md.update(host_samples, n * 4);
-        } else {
-            const int w = aligned == 24 ? 3 : 4;
-            std::vector<uint8_t> tmp(4096 * 4);
-            for (uint64_t i = 0; i < n; i += 4096) {
-                const uint64_t m = std::min<uint64_t>(4096, n - i);
+        uint8_t tmp[4096 * 4];
+        for (uint64_t i = 0; i < n; i += 4096) {
+            const uint64_t m = std::min<uint64_t>(4096, n - i);
+            if (kind_ == 1) {
+                const int16_t* v = static_cast<const int16_t*>(samples) + i;
+                int16_t* t = reinterpret_cast<int16_t*>(tmp);
+                for (uint64_t k = 0; k < m; k++) t[k] = (int16_t)(v[k] >> js_);
+                md_.update(tmp, m * 2);
+            } else {
+                const int32_t* v = static_cast<const int32_t*>(samples) + i;
+                const int w = w24_ ? 3 : 4;
                 for (uint64_t k = 0; k < m; k++) {
-                    const uint32_t x = (uint32_t)(v[i + k] >> js);
+                    const uint32_t x = (uint32_t)(v[k] >> js_);
                     for (int bb = 0; bb < w; bb++) tmp[k * w + bb] = (uint8_t)(x >> (8 * bb));
                 }
-                md.update(tmp.data(), m * w);
+                md_.update(tmp, m * w);
             }
         }
     }
-    uint8_t dig[16];
-    md.finish(dig);
-    return std::memcmp(dig, s.si.md5, 16) == 0;
+    bool matches(const uint8_t* expected) {
+        uint8_t dig[16];
+        md_.finish(dig);
+        return std::memcmp(dig, expected, 16) == 0;
+    }
+
+private:
+    Md5 md_;
+    int kind_;
+    uint32_t js_;
+    bool w24_;
+};
+
+bool md5_matches(const StreamState& s, const void* host_samples) {
+    SampleHasher h(s);
+    h.update(host_samples, s.info.n_samples);
+    return h.matches(s.si.md5);
+}
+
+// D2H of one stream's samples into caller memory, with the STREAMINFO MD5 when `hash`.
+// Long streams: the calling thread copies chunk after chunk while a helper thread hashes
+// every chunk already landed, so the call costs about max(D2H, MD5) instead of their sum.
+int read_samples(zflac_batch* b, StreamState& s, void* out, bool hash) {
+    const uint64_t bytes = s.info.samples_bytes;
+    const uint64_t esz = (uint64_t)esz_of_kind(s.kind);
+    constexpr uint64_t CHUNK = 32ull << 20;  // a multiple of every element size
+    const double t0 = now_ms();
+    double t_md5 = 0;
+    bool ok = true;
+    if (!hash || bytes <= 2 * CHUNK) {
+        if (bytes) ck(hipMemcpy(out, s.dev_samples, bytes, hipMemcpyDeviceToHost));
+        if (hash) {
+            const double t1 = now_ms();
+            ok = md5_matches(s, out);
+            t_md5 = now_ms() - t1;
+        }
+    } else {
+        std::atomic<uint64_t> landed{0};
+        std::thread hasher([&] {
+            const double h0 = now_ms();
+            SampleHasher h(s);
+            uint64_t done = 0;
+            while (done < bytes) {
+                const uint64_t l = landed.load(std::memory_order_acquire);
+                if (l == done) {
+                    std::this_thread::yield();
+                    continue;
+                }
+                h.update(static_cast<const uint8_t*>(out) + done, (l - done) / esz);
+                done = l;
+            }
+            ok = h.matches(s.si.md5);
+            t_md5 = now_ms() - h0;
+        });
+        hipError_t e = hipSuccess;
+        for (uint64_t off = 0; off < bytes; off += CHUNK) {
+            const uint64_t len = std::min(CHUNK, bytes - off);
+            if (e == hipSuccess)
+                e = hipMemcpy(static_cast<uint8_t*>(out) + off, static_cast<const uint8_t*>(s.dev_samples) + off, len,
+                              hipMemcpyDeviceToHost);
+            landed.store(off + len, std::memory_order_release);  // on failure: drain the hasher
+        }
+        hasher.join();
+        ck(e);
+    }
+    b->timings.read_ms = now_ms() - t0;
+    b->timings.host_md5_ms = t_md5;
+    return ok ? E_OK : E_INVALID_CHECKSUM;
 }
 
 // STREAMINFO MD5 of every decoded stream on the device (k_md5, one lane per stream),
@@ -905,11 +1038,14 @@ int create_batch(const zflac_stream* streams, size_t n, int device, int flags, z
         // timing-only events: no system-scope fence (cache writeback + invalidate) at each
         // record, which would otherwise slow the kernel after it
         for (auto& e : b->ev) ck(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+        const double t0 = now_ms();
         b->streams.resize(n);
         for (size_t i = 0; i < n; i++) {
             if (!streams[i].data && streams[i].len) return E_INVALID_ARGUMENT;
             plan_stream(b->streams[i], streams[i].data, streams[i].len);
         }
+        const double t1 = now_ms();
+        b->timings.plan_ms = t1 - t0;
         for (size_t i = 0; i < n; i++) {
             StreamState& s = b->streams[i];
             if (s.host_err || s.no_frames) continue;
@@ -926,6 +1062,7 @@ int create_batch(const zflac_stream* streams, size_t n, int device, int flags, z
             b->classes[ci]->members.push_back((uint32_t)i);
         }
         for (auto& C : b->classes) alloc_class(b.get(), *C, streams);
+        b->timings.upload_ms = now_ms() - t1;
         // streams resolved on the host
         for (auto& s : b->streams) {
             if (s.host_err) s.err = s.host_err;
@@ -992,7 +1129,9 @@ int zflac_hip_batch_run(zflac_batch* b) {
     if (!b) return E_INVALID_ARGUMENT;
     b->ran = false;
     try {
+        const double t0 = now_ms();
         run_batch(b);
+        b->timings.run_wall_ms = now_ms() - t0;
         b->ran = true;
     } catch (const DeviceError&) {
         return E_DEVICE;
@@ -1023,14 +1162,11 @@ int zflac_hip_batch_read(zflac_batch* b, size_t i, void* out, size_t out_bytes, 
     if (out_bytes < s.info.samples_bytes || (!out && s.info.samples_bytes)) return E_INVALID_ARGUMENT;
     try {
         ck(hipSetDevice(b->device));
-        if (s.info.samples_bytes)
-            ck(hipMemcpy(out, s.dev_samples, s.info.samples_bytes, hipMemcpyDeviceToHost));
+        // a device verdict stands in for the host hash (a mismatch is already s.err)
+        return read_samples(b, s, out, verify_md5 && !s.md5_dev);  // InvalidChecksum at :279-280
     } catch (const DeviceError&) {
         return E_DEVICE;
     }
-    // a device verdict stands in for the host hash (a mismatch is already s.err)
-    if (verify_md5 && !s.md5_dev && !md5_matches(s, out)) return E_INVALID_CHECKSUM;  // :279-280
-    return E_OK;
 }
 
 int zflac_hip_batch_md5(zflac_batch* b, size_t i, uint8_t* digest) {
@@ -1043,7 +1179,7 @@ int zflac_hip_batch_md5(zflac_batch* b, size_t i, uint8_t* digest) {
 
 int zflac_hip_batch_timings(zflac_batch* b, zflac_timings* t) {
     if (!b || !t) return E_INVALID_ARGUMENT;
-    *t = b->timings;
+    *t = b->timings;  // the host wall-clock fields are always filled
     return b->have_timing ? E_OK : E_INVALID_ARGUMENT;
 }
 
