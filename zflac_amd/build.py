@@ -29,11 +29,15 @@ def _obj_deps(src: str):
     return [src] + hdrs + [os.path.join(ROOT, "include", "zflac_hip.h")]
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, defines=(), out: str | None = None) -> str:
+    """Build libzflac_hip.so (or, with `out`, a variant with extra -D `defines` for timing
+    experiments: separate object directory, never the product library)."""
+    lib = out or LIB
+    if not force and not defines and not out and not needs_build():
         return LIB
     objs = []
-    build_dir = os.path.join(HERE, "_build")
+    tag = "_".join(d.replace("=", "-") for d in defines)
+    build_dir = os.path.join(HERE, "_build" + ("_" + tag if tag else ""))
     os.makedirs(build_dir, exist_ok=True)
     procs = []
     for src in SOURCES:  # translation units compile in parallel; up-to-date objects are kept
@@ -44,6 +48,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
             continue
         cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-Wall",
                "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+        cmd[1:1] = [f"-D{d}" for d in defines]
         if src.endswith(".hip"):
             cmd[1:1] = ["-x", "hip"]
         if verbose:
@@ -53,10 +58,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
     failed = [src for src, p in procs if p.wait() != 0]
     if failed:
         raise RuntimeError(f"hipcc failed for {failed}")
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs
     subprocess.check_call(cmd)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose=True)
+    # python -m zflac_amd.build [--force] [-DNAME ...] [-o out.so]
+    a = sys.argv[1:]
+    out = a[a.index("-o") + 1] if "-o" in a else None
+    build(force="--force" in a, verbose=True, defines=[x[2:] for x in a if x.startswith("-D")], out=out)
