@@ -31,6 +31,16 @@ __global__ __launch_bounds__(THREADS) void k_write_private(uint4* __restrict__ o
     for (uint32_t q = 0; q < LANE_BYTES / 16; q++) p[q] = make_uint4(lane, q, lane ^ q, 7);
 }
 
+// The staged write-back of k_decode's stereo fast path: every group of 8 lanes stores one
+// frame's 128 contiguous bytes per chunk (lane L: 16 B at run + (L & 7) * 16), frames far
+// apart (one region per lane group, like one output region per frame).
+__global__ __launch_bounds__(THREADS) void k_write_runs(uint4* __restrict__ out) {
+    const uint32_t lane = blockIdx.x * THREADS + threadIdx.x;
+    const uint32_t group = lane >> 3, piece = lane & 7;
+    uint4* p = out + (uint64_t)group * (8 * LANE_BYTES / 16) + piece;
+    for (uint32_t q = 0; q < 8 * LANE_BYTES / 16; q += 8) p[q] = make_uint4(lane, q, lane ^ q, 7);
+}
+
 __global__ __launch_bounds__(THREADS) void k_read_coalesced(const uint4* __restrict__ in, uint32_t* __restrict__ sink,
                                                             uint64_t nq) {
     uint32_t acc = 0;
@@ -61,11 +71,13 @@ int main() {
     for (int it = 0; it < 3; it++) {
         k_read_private<<<blocks, THREADS>>>(buf, sink);
         k_write_private<<<blocks, THREADS>>>(buf);
+        k_write_runs<<<blocks, THREADS>>>(buf);
         k_read_coalesced<<<4096, THREADS>>>(buf, sink, bytes / 16);
     }
     CK(hipDeviceSynchronize());
-    printf("{\"read_private_bytes\": %llu, \"write_private_bytes\": %llu, \"read_coalesced_bytes\": %llu}\n",
-           (unsigned long long)bytes, (unsigned long long)bytes, (unsigned long long)bytes);
+    printf("{\"read_private_bytes\": %llu, \"write_private_bytes\": %llu, \"write_runs_bytes\": %llu, "
+           "\"read_coalesced_bytes\": %llu}\n",
+           (unsigned long long)bytes, (unsigned long long)bytes, (unsigned long long)bytes, (unsigned long long)bytes);
     CK(hipFree(buf));
     CK(hipFree(sink));
     return 0;

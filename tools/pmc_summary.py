@@ -37,18 +37,29 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--json")
+    ap.add_argument("--lib", help="library the counters were taken on (default: the in-tree build)")
+    ap.add_argument("--store-pattern", choices=["runs", "private"], default="runs",
+                    help="store pattern of the decode kernel: staged 128-B runs (16-bit stereo) or per-lane")
     a = ap.parse_args()
     calib = load(os.path.join(a.dir, "calib_FETCH_SIZE"))
     calib_w = load(os.path.join(a.dir, "calib_WRITE_SIZE"))
     nbytes = 5242880000.0  # tools/calib_pmc.hip: LANE_BYTES * LANES
-    f_read = w_write = None
+    f_read = w_write = w_runs = None
     for k, v in calib.items():
         if "k_read_private" in k:
             f_read = nbytes / (sum(v["FETCH_SIZE"]) / len(v["FETCH_SIZE"]) * 1024)
     for k, v in calib_w.items():
         if "k_write_private" in k:
             w_write = nbytes / (sum(v["WRITE_SIZE"]) / len(v["WRITE_SIZE"]) * 1024)
-    out = {"calibration": {"fetch_factor_private_16B": f_read, "write_factor_private_16B": w_write}, "kernels": {}}
+        if "k_write_runs" in k:
+            w_runs = nbytes / (sum(v["WRITE_SIZE"]) / len(v["WRITE_SIZE"]) * 1024)
+    lib = a.lib or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "zflac_amd",
+                                "libzflac_hip.so")
+    import hashlib
+
+    out = {"calibration": {"fetch_factor_private_16B": f_read, "write_factor_private_16B": w_write,
+                           "write_factor_runs_128B": w_runs},
+           "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(), "_source": a.dir, "kernels": {}}
     runs = [d for d in sorted(glob.glob(os.path.join(a.dir, "p*"))) if os.path.isdir(d)]
     merged = defaultdict(dict)
     for d in runs:
@@ -59,8 +70,9 @@ def main():
         row = dict(cs)
         if "FETCH_SIZE" in cs and f_read:
             row["hbm_read_bytes"] = cs["FETCH_SIZE"] * 1024 * f_read
-        if "WRITE_SIZE" in cs and w_write:
-            row["hbm_write_bytes"] = cs["WRITE_SIZE"] * 1024 * w_write
+        wf = w_runs if a.store_pattern == "runs" else w_write
+        if "WRITE_SIZE" in cs and wf:
+            row["hbm_write_bytes"] = cs["WRITE_SIZE"] * 1024 * wf
         if "hbm_read_bytes" in row and "hbm_write_bytes" in row:
             row["hbm_traffic_bytes"] = row["hbm_read_bytes"] + row["hbm_write_bytes"]
         w = cs.get("SQ_WAVES")

@@ -118,6 +118,8 @@ struct DecodeArgs {
     int write;
     void* dummy;  // DUMMY_BYTES: target of masked-off / pending-less packed stores
     uint32_t* sub_start;  // [frame][MAX_CH]: bit offset of subframe c >= 1 (k_walk -> k_decode)
+    uint32_t* group_mb;   // [frame group of a k_decode wave]: its history bucket, written by the
+                          // first bucket launch so the later launches skip other groups cheaply
 };
 
 // One stream for k_md5 (md5.hip): the message is the decoded samples before left-justify,

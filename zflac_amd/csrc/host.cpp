@@ -275,7 +275,7 @@ struct Class {
     DevBuf<unsigned long long> chunk_units, chunk_uoff;
     DevBuf<uint64_t> chunk_slots;
     DevBuf<uint64_t> c_pos, c_out, c_end;
-    DevBuf<uint32_t> c_stream, c_info, c_rate, sub;
+    DevBuf<uint32_t> c_stream, c_info, c_rate, sub, group_mb;
     DevBuf<int32_t> c_err;
     DevBuf<uint8_t> dummy;  // sink of masked-off packed stores (64 lanes x 32 B)
     // pinned host mirror, so the per-run read-backs are plain DMA on the batch stream:
@@ -514,6 +514,7 @@ void alloc_candidates(Class& C) {
     C.c_rate.alloc(C.cap);
     C.c_err.alloc(C.cap);
     C.sub.alloc((size_t)C.cap * MAX_CH);
+    C.group_mb.alloc((size_t)C.cap / 4 + 2);  // one per k_decode frame group (>= 8 frames each)
 }
 
 DecodeArgs decode_args(Class& C) {
@@ -536,6 +537,7 @@ DecodeArgs decode_args(Class& C) {
     a.write = 1;
     a.dummy = C.dummy.p;
     a.sub_start = C.sub.p;
+    a.group_mb = C.group_mb.p;
     return a;
 }
 
@@ -616,7 +618,7 @@ struct SeqRunner {
     DevBuf<uint64_t> p_pos, p_out, p_end;
     DevBuf<uint32_t> p_stream, p_info, p_rate;
     DevBuf<int32_t> p_err;
-    DevBuf<uint32_t> p_sub;
+    DevBuf<uint32_t> p_sub, p_mb;
     DevBuf<StreamDesc> p_desc;
 
     SeqRunner(zflac_batch* b_, Class& C_, uint32_t slot_) : b(b_), C(C_), slot(slot_) {}
@@ -661,6 +663,8 @@ struct SeqRunner {
         a.dummy = C.dummy.p;
         p_sub.alloc(n * MAX_CH);
         a.sub_start = p_sub.p;
+        p_mb.alloc(n / 4 + 2);
+        a.group_mb = p_mb.p;
         ck(launch_decode(C.kind, a, (uint32_t)n, st));
         std::vector<uint64_t> e(n);
         std::vector<int32_t> er(n);
