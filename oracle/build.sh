@@ -1,5 +1,7 @@
 #!/bin/sh
 # Build the CPU oracle (test infrastructure). Outputs stay under oracle/_build/ (git-ignored).
+# tests/test_oracle_sanitized.py builds the checked flavour again with ASan + UBSan
+# (sanitize_main.c) and runs it over every test stream.
 set -e
 cd "$(dirname "$0")"
 mkdir -p _build

@@ -166,7 +166,7 @@ def md5_message(pcm: np.ndarray, bps: int) -> bytes:
     return np.ascontiguousarray(b[:, :3] if a == 3 else b).tobytes()
 
 
-def tile_flac(st: Stream, reps: int) -> bytes:
+def tile_flac(st: Stream, reps: int, unknown_total: bool = False) -> bytes:
     """`st` with its frame section repeated `reps` times: a long stream for throughput
     runs without generating every frame (LPC analysis is the slow part of the writer).
     STREAMINFO's total samples and MD5 are rewritten for the repeated PCM, so decode()
@@ -181,7 +181,7 @@ def tile_flac(st: Stream, reps: int) -> bytes:
     d = bytearray(st.flac[: st.frames_begin])
     assert d[:4] == b"fLaC" and (d[4] & 0x7F) == 0
     o = 8
-    total = int(st.pcm.size // cfg["channels"]) * reps
+    total = 0 if unknown_total else int(st.pcm.size // cfg["channels"]) * reps
     if total >= 1 << 36:
         raise ValueError("tile_flac: total samples exceed STREAMINFO's 36 bits")
     d[o + 13] = (d[o + 13] & 0xF0) | ((total >> 32) & 15)
