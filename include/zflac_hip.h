@@ -45,6 +45,7 @@ extern "C" {
 #define ZFLAC_E_DEVICE 13                   /* HIP runtime failure / no GPU (no zflac equivalent) */
 #define ZFLAC_E_INVALID_ARGUMENT 14         /* bad handle, index or buffer size */
 #define ZFLAC_E_OUT_OF_DOMAIN 15            /* input on which Debug zflac traps */
+#define ZFLAC_E_FRAME_CRC 16                /* frame CRC-16 mismatch, only with ZFLAC_FLAG_CHECK_CRC16 */
 
 /* Arm of zflac's `Samples` union (src/zflac.zig:12-16). */
 #define ZFLAC_S8 0
@@ -87,6 +88,7 @@ typedef struct zflac_timings {
     double run_wall_ms; /* last batch_run, launch to results (kernels + read-backs) */
     double read_ms;     /* last batch_read / read: D2H of the samples (+ MD5 overlapped) */
     double host_md5_ms; /* last batch_read / read: host STREAMINFO MD5 (overlapped with the D2H) */
+    double crc16_ms;    /* k_crc16 of the last run (ZFLAC_FLAG_CHECK_CRC16 with ZFLAC_FLAG_TIMING), else 0 */
 } zflac_timings;
 
 typedef struct zflac_batch zflac_batch;
@@ -97,6 +99,9 @@ typedef struct zflac_batch zflac_batch;
  * then call zflac_hip_read). The returned code is the zflac error of the stream
  * (MD5 is checked by zflac_hip_read). */
 int zflac_hip_open(const uint8_t *buf, size_t len, int device, zflac_batch **out_batch, zflac_info *info);
+/* zflac_hip_open with batch flags (ZFLAC_FLAG_CHECK_CRC16, ZFLAC_FLAG_TIMING). */
+int zflac_hip_open_ex(const uint8_t *buf, size_t len, int device, int flags, zflac_batch **out_batch,
+                      zflac_info *info);
 /* Copy the samples into caller memory, verify the STREAMINFO MD5
  * (ZFLAC_E_INVALID_CHECKSUM on mismatch, as src/zflac.zig:279-280), left-justify is
  * already applied on the device (src/zflac.zig:287-306). Long streams are copied back in
@@ -139,6 +144,12 @@ void zflac_hip_batch_destroy(zflac_batch *b);
  * the host, which zflac_hip_read / zflac_hip_batch_read do without this flag). A
  * mismatch makes the stream's result ZFLAC_E_INVALID_CHECKSUM (src/zflac.zig:279-280). */
 #define ZFLAC_FLAG_DEVICE_MD5 4
+/* Check every decoded frame's CRC-16 trailer on the device (k_crc16). zflac reads the
+ * trailer and ignores it (src/zflac.zig:548-551), so this is off by default; with it, the
+ * first frame in stream order whose trailer differs makes the stream ZFLAC_E_FRAME_CRC
+ * (ahead of a later frame's error and of the MD5 check, which come after it in zflac's
+ * read order). */
+#define ZFLAC_FLAG_CHECK_CRC16 8
 
 const char *zflac_hip_error_name(int code);
 /* Number of HIP devices visible; 0 means every decode will fail with ZFLAC_E_DEVICE. */

@@ -21,6 +21,7 @@ ERROR_NAMES = {
     5: "InvalidChecksum", 6: "InvalidFrameHeader", 7: "InconsistentParameters", 8: "InvalidCodedNumber",
     9: "InvalidSubframeHeader", 10: "InvalidResidualCodingMethod", 11: "EndOfStream", 12: "OutOfMemory",
     13: "DeviceError", 14: "InvalidArgument", 15: "OutOfDomain",
+    16: "FrameCrcMismatch",  # never returned here: zflac ignores the CRC-16 trailer (src/zflac.zig:548-551)
 }
 _KIND_DTYPE = {0: np.int8, 1: np.int16, 2: np.int32}
 

@@ -1,15 +1,16 @@
-"""Per-config throughput on one GPU beside the CPU oracle (BASELINE.md's table).
+"""Per-config throughput on one GPU beside the CPU oracle (BASELINE.md's table, SURVEY.md
+8(d) sizes), plus the format rows of SURVEY.md 8(f)4 and the repair paths.
 
-For each BASELINE.json config that runs on one GPU (C2 mono fixed-2, C3 mid/side LPC-8,
-C4 24-bit LPC-32 with wasted bits: one long stream each; C3 also as a 1250-stream batch
-is bench.py's workload) this decodes the stream with the HIP path, inputs resident in HBM,
-and reports:
-  * gpu_msps: channel-samples / wall time of one device-resident run (scan..verify);
-  * kernel times (scan+compact, walk, decode) from the library's HIP events;
-  * cpu_1t_msps: the oracle's ReleaseFast-like build on one host thread, same stream
-    (zflac decodes one stream on one thread), MD5 included;
-  * bit_exact: every run's PCM hashes to the STREAMINFO MD5, and equals the oracle.
-Usage (GPU box): python tools/bench_configs.py [--frames N] [--out file.json]
+For each row one stream (a seeded segment repeated to the row's frame count with
+synth.tile_flac: every frame is decoded and the STREAMINFO MD5 covers the whole output):
+  * device_msps: channel-samples / wall time of one device-resident zflac_hip_batch_run
+    (inputs in HBM, scan .. verify), and its kernel times (HIP events);
+  * e2e_msps: the drop-in decode(): zflac_hip_open + zflac_hip_read (upload, device
+    decode, copy back overlapped with the host STREAMINFO MD5), best of 2;
+  * oracle_1t_msps: the oracle's ReleaseFast-like build on one host thread (zflac decodes
+    one stream on one thread), MD5 included, timed on the segment and scaled by the repeats;
+  * bit_exact: decode() verified the whole-stream MD5 and the segment equals the oracle.
+Usage (GPU box): python tools/bench_configs.py [--rows a,b] [--out file.json]
 """
 from __future__ import annotations
 
@@ -28,12 +29,38 @@ import oracle  # noqa: E402  (CPU baseline and checker only)
 import synth  # noqa: E402
 import zflac_amd  # noqa: E402
 
+B = 4096
+ROWS = {
+    # name: (flacgen config of one segment, segment frames, total frames, unknown total)
+    "C2 mono 16-bit fixed-2 k=4": (synth.config_c2(), 1024, 65536, False),
+    "C3 stereo M/S 16-bit LPC-8": (synth.config_c3(), 1024, 65536, False),
+    "C4 stereo 24-bit LPC-32 shift 15 wasted 4": (synth.config_c4(), 512, 65536, False),
+    "verbatim stereo 16-bit": (dict(channels=2, bps=16, predictor=0, stereo_mode=1, block_size=B), 256, 4096, False),
+    "constant-heavy stereo 16-bit": (dict(channels=2, bps=16, stereo_mode=1, silence_every=1, block_size=B), 256, 4096,
+                                     False),
+    "mono 8-bit LPC-4": (dict(channels=1, bps=8, order=4, precision=7, block_size=B, noise_lsb=1.0, tone_amp=0.3), 256,
+                         4096, False),
+    "stereo 12-bit M/S LPC-8": (dict(channels=2, bps=12, stereo_mode=10, order=8, block_size=B, noise_lsb=4.0), 256,
+                                4096, False),
+    "stereo 20-bit M/S LPC-12": (dict(channels=2, bps=20, stereo_mode=10, order=12, precision=14, block_size=B,
+                                      noise_lsb=16.0), 256, 4096, False),
+    "stereo 32-bit LPC-8": (dict(channels=2, bps=32, stereo_mode=1, order=8, precision=15, block_size=B, tone_amp=0.2,
+                                 noise_lsb=1e6), 256, 4096, False),
+    "6-channel 24-bit LPC-10": (dict(channels=6, bps=24, order=10, precision=14, block_size=B, noise_lsb=64.0), 128,
+                                2048, False),
+    "C3, total unknown (sequential planner)": (synth.config_c3(), 256, 4096, True),
+    "C3, planted false syncs (repair path)": (dict(channels=2, bps=16, stereo_mode=1, order=8, block_size=B,
+                                                   plant_sync_every=2), 256, 4096, False),
+}
 
-def run_config(name, cfg, steps, cpu_seconds):
-    t0 = time.perf_counter()
-    st = synth.generate(**cfg)
-    gen_s = time.perf_counter() - t0
-    b = zflac_amd.Batch([st.flac], timing=True)
+
+def run_row(name, cfg, seg, frames, unknown, steps):
+    st = synth.generate(**dict(cfg, n_samples=B * seg, seed=cfg.get("seed", 7)))
+    reps = max(1, frames // seg)
+    data = synth.tile_flac(st, reps, unknown_total=unknown)
+    n = st.pcm.size * reps
+    # device-resident batch runs
+    b = zflac_amd.Batch([data], timing=True)
     for _ in range(2):
         b.run()
     walls, tms = [], []
@@ -42,54 +69,59 @@ def run_config(name, cfg, steps, cpu_seconds):
         b.run()
         walls.append(time.perf_counter() - t)
         tms.append(b.timings())
-    d = b.read(0, verify_md5=True)  # raises InvalidChecksum on a mismatch
-    ref = oracle.decode(st.flac, "fast")
-    exact = ref.error == "OK" and np.array_equal(d.samples.values, ref.samples)
-    n = d.samples.values.size
     b.close()
-    # CPU: the oracle, one thread, whole stream decodes for ~cpu_seconds
-    reps, t_cpu = 0, 0.0
-    while t_cpu < cpu_seconds or reps == 0:
+    # decode() end to end (raises InvalidChecksum unless the whole output is bit-exact)
+    best, tm = None, {}
+    for _ in range(2):
+        cur = {}
+        t0 = time.perf_counter()
+        d = zflac_amd.decode(data, timings=cur)
+        w = time.perf_counter() - t0
+        if best is None or w < best:
+            best, tm = w, cur
+        assert d.samples.values.size == n
+    seg_ref = oracle.decode(st.flac, "fast")
+    exact = seg_ref.error == "OK" and np.array_equal(d.samples.values[: seg_ref.samples.size], seg_ref.samples)
+    del d
+    # oracle, one thread, on the segment
+    reps_cpu, t_cpu = 0, 0.0
+    while t_cpu < 1.0 or reps_cpu == 0:
         t = time.perf_counter()
-        err, ns = oracle.decode_count_only(st.flac)
+        err, ns = oracle.decode_count_only(st.flac, "fast")
         t_cpu += time.perf_counter() - t
-        reps += 1
-        assert err == 0 and ns == n
+        reps_cpu += 1
+        assert err == 0
+    cpu_msps = st.pcm.size * reps_cpu / t_cpu / 1e6
     wall = float(np.median(walls))
+    mean = lambda f: round(float(np.mean([f(t) for t in tms])), 4)  # noqa: E731
     return {
-        "config": name, "channel_samples": int(n), "compressed_bytes": len(st.flac),
-        "bytes_per_sample_alg": round((len(st.flac) + d.samples.values.nbytes) / n, 3),
-        "gpu_msps": round(n / wall / 1e6, 1), "gpu_wall_ms": round(wall * 1e3, 3),
-        "scan_ms": round(float(np.mean([t.scan_ms for t in tms])), 4),
-        "walk_ms": round(float(np.mean([t.walk_ms for t in tms])), 4),
-        "decode_ms": round(float(np.mean([t.decode_ms for t in tms])), 4),
-        "decode_kernel_msps": round(n / (float(np.mean([t.decode_ms + t.walk_ms for t in tms])) * 1e-3) / 1e6, 1),
-        "cpu_1t_msps": round(n * reps / t_cpu / 1e6, 1), "cpu_sample": f"{reps} whole-stream decodes, 1 thread",
-        "gpu_over_cpu_1t": round((n / wall) / (n * reps / t_cpu), 1),
-        "bit_exact": bool(exact), "gen_seconds": round(gen_s, 2),
+        "row": name, "frames": seg * reps, "channel_samples": int(n), "compressed_bytes": len(data),
+        "device_msps": round(n / wall / 1e6, 1), "device_wall_ms": round(wall * 1e3, 3),
+        "scan_ms": mean(lambda t: t.scan_ms), "walk_ms": mean(lambda t: t.walk_ms),
+        "decode_ms": mean(lambda t: t.decode_ms), "verify_ms": mean(lambda t: t.verify_ms),
+        "e2e_msps": round(n / best / 1e6, 1), "e2e_ms": round(best * 1e3, 1),
+        "e2e_breakdown_ms": {k: round(tm[k], 2) for k in ("upload_ms", "run_wall_ms", "read_ms", "host_md5_ms")},
+        "oracle_1t_msps": round(cpu_msps, 1), "device_over_oracle_1t": round(n / wall / 1e6 / cpu_msps, 1),
+        "e2e_over_oracle_1t": round(n / best / 1e6 / cpu_msps, 2), "bit_exact": bool(exact),
     }
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--frames", type=int, default=4096, help="frames per stream (block 4096)")
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--cpu-seconds", type=float, default=3.0)
+    ap.add_argument("--rows", help="comma-separated substrings of row names (default: all)")
+    ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--out")
     a = ap.parse_args()
-    cfgs = {
-        "C2 mono 16-bit fixed-2 k=4": synth.config_c2(n_frames=a.frames),
-        "C3 stereo mid/side 16-bit LPC-8": synth.config_c3(n_frames=a.frames),
-        "C4 stereo 24-bit LPC-32 shift 15, 4 wasted bits": synth.config_c4(n_frames=a.frames),
-    }
+    sel = [r for r in ROWS if not a.rows or any(x in r for x in a.rows.split(","))]
     rows = []
-    for name, cfg in cfgs.items():
-        r = run_config(name, cfg, a.steps, a.cpu_seconds)
+    for name in sel:
+        cfg, seg, frames, unknown = ROWS[name]
+        r = run_row(name, cfg, seg, frames, unknown, a.steps)
         print(json.dumps(r), flush=True)
         rows.append(r)
     if a.out:
         with open(a.out, "w") as f:
-            json.dump({"frames_per_stream": a.frames, "rows": rows}, f, indent=1)
+            json.dump({"rows": rows}, f, indent=1)
     if not all(r["bit_exact"] for r in rows):
         sys.exit(1)
 

@@ -29,7 +29,8 @@ class zflac_timings(ctypes.Structure):
                 ("total_ms", ctypes.c_double), ("frames", ctypes.c_uint64), ("input_bytes", ctypes.c_uint64),
                 ("output_bytes", ctypes.c_uint64), ("samples", ctypes.c_uint64), ("walk_ms", ctypes.c_double),
                 ("md5_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("upload_ms", ctypes.c_double),
-                ("run_wall_ms", ctypes.c_double), ("read_ms", ctypes.c_double), ("host_md5_ms", ctypes.c_double)]
+                ("run_wall_ms", ctypes.c_double), ("read_ms", ctypes.c_double), ("host_md5_ms", ctypes.c_double),
+                ("crc16_ms", ctypes.c_double)]
 
 
 # every symbol include/zflac_hip.h declares, with (restype, argtypes)
@@ -37,6 +38,8 @@ _P = ctypes.c_void_p
 SIGNATURES = {
     "zflac_hip_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(_P),
                                       ctypes.POINTER(zflac_info)]),
+    "zflac_hip_open_ex": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                         ctypes.POINTER(_P), ctypes.POINTER(zflac_info)]),
     "zflac_hip_read": (ctypes.c_int, [_P, _P, ctypes.c_size_t]),
     "zflac_hip_close": (None, [_P]),
     "zflac_hip_batch_create": (ctypes.c_int, [ctypes.POINTER(zflac_stream), ctypes.c_size_t, ctypes.c_int,
@@ -57,6 +60,7 @@ SIGNATURES = {
 FLAG_TIMING = 1
 FLAG_FORCE_SLOW = 2
 FLAG_DEVICE_MD5 = 4
+FLAG_CHECK_CRC16 = 8  # beyond zflac (src/zflac.zig:548-551 ignores the trailer)
 
 _lib = None
 

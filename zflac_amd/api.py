@@ -73,14 +73,17 @@ def _aligned_empty(nbytes: int, dtype) -> np.ndarray:
     return raw[off:off + nbytes].view(dtype)
 
 
-def decode(reader, device: int = 0, timings: dict | None = None) -> DecodedFLAC:
+def decode(reader, device: int = 0, timings: dict | None = None, check_crc16: bool = False) -> DecodedFLAC:
     """Decode one FLAC stream on `device`; raises zflac-named errors (errors.*).
-    `timings` (a dict) receives the library's host wall-clock breakdown of the call."""
+    `timings` (a dict) receives the library's host wall-clock breakdown of the call.
+    `check_crc16` also checks every frame's CRC-16 trailer on the device (FrameCrcMismatch);
+    zflac itself ignores it (src/zflac.zig:548-551)."""
     data = _read_all(reader)
     L = _lib.load()
     handle = ctypes.c_void_p()
     info = _lib.zflac_info()
-    rc = L.zflac_hip_open(data, len(data), device, ctypes.byref(handle), ctypes.byref(info))
+    flags = _lib.FLAG_CHECK_CRC16 if check_crc16 else 0
+    rc = L.zflac_hip_open_ex(data, len(data), device, flags, ctypes.byref(handle), ctypes.byref(info))
     try:
         errors.check(rc)
         out = _aligned_empty(info.samples_bytes, _DTYPES[info.sample_kind])
@@ -105,7 +108,7 @@ class Batch:
     """
 
     def __init__(self, streams, device: int = 0, timing: bool = False, force_slow: bool = False,
-                 device_md5: bool = False):
+                 device_md5: bool = False, check_crc16: bool = False):
         self._L = _lib.load()
         self._bufs = [bytes(s) for s in streams]
         arr = (_lib.zflac_stream * len(self._bufs))()
@@ -116,7 +119,7 @@ class Batch:
             arr[i].data = ctypes.cast(cb, ctypes.c_void_p)
             arr[i].len = len(b)
         flags = ((_lib.FLAG_TIMING if timing else 0) | (_lib.FLAG_FORCE_SLOW if force_slow else 0)
-                 | (_lib.FLAG_DEVICE_MD5 if device_md5 else 0))
+                 | (_lib.FLAG_DEVICE_MD5 if device_md5 else 0) | (_lib.FLAG_CHECK_CRC16 if check_crc16 else 0))
         self._h = ctypes.c_void_p()
         rc = self._L.zflac_hip_batch_create(arr, len(self._bufs), device, flags, ctypes.byref(self._h))
         self._keep = None  # the library copied the bytes to HBM

@@ -4,13 +4,15 @@ from __future__ import annotations
 import os
 import subprocess
 import sys
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libzflac_hip.so")
-SOURCES = [os.path.join(CSRC, f"decode_k{k}_{lay}.hip") for k in (1, 2, 0) for lay in ("stereo", "mono", "multi")]
-SOURCES += [os.path.join(CSRC, n) for n in ("scan.hip", "md5.hip", "host.cpp")]
+SOURCES = [os.path.join(CSRC, f"decode_k{k}_{lay}{mix}.hip") for k in (1, 2, 0) for lay in ("stereo", "mono", "multi")
+           for mix in ("", "_mix")]
+SOURCES += [os.path.join(CSRC, n) for n in ("scan.hip", "md5.hip", "crc16.hip", "host.cpp")]
 HEADERS = [os.path.join(CSRC, n) for n in ("common.h", "md5.hpp", "device_common.h", "decode.inc")]
 DEPS = SOURCES + HEADERS + [os.path.join(ROOT, "include", "zflac_hip.h")]
 ARCH = os.environ.get("ZFLAC_OFFLOAD_ARCH", "gfx950")
@@ -40,6 +42,7 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
     build_dir = os.path.join(HERE, "_build" + ("_" + tag if tag else ""))
     os.makedirs(build_dir, exist_ok=True)
     procs = []
+    jobs = max(1, min(int(os.environ.get("MAX_JOBS", "8")), os.cpu_count() or 1, 16))
     for src in SOURCES:  # translation units compile in parallel; up-to-date objects are kept
         obj = os.path.join(build_dir, os.path.basename(src) + ".o")
         if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d)
@@ -53,6 +56,8 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
             cmd[1:1] = ["-x", "hip"]
         if verbose:
             print(" ".join(cmd))
+        while sum(p.poll() is None for _, p in procs) >= jobs:  # bounded: each decode unit is GBs of RAM
+            time.sleep(0.2)
         procs.append((src, subprocess.Popen(cmd)))
         objs.append(obj)
     failed = [src for src, p in procs if p.wait() != 0]

@@ -22,6 +22,7 @@ enum Err : int {
     E_DEVICE = 13,
     E_INVALID_ARGUMENT = 14,
     E_OUT_OF_DOMAIN = 15,
+    E_FRAME_CRC = 16,  // frame CRC-16 mismatch: only with ZFLAC_FLAG_CHECK_CRC16 (zflac never checks it)
 };
 
 // One stream of a batch, as the kernels see it. Byte offsets are absolute in the
@@ -154,6 +155,20 @@ struct VerifyArgs {
     const uint32_t* c_info;
     const uint32_t* c_rate;
     uint32_t* status;           // per stream: nonzero => take the sequential path
+};
+
+// k_crc16 (crc16.hip): frame f covers bytes [pos[f], end[f] - 2) with its CRC-16 trailer at
+// end[f] - 2 (c_end as k_decode records it). Frames with err[f] != 0 are skipped.
+struct Crc16Args {
+    const uint8_t* in;
+    uint64_t in_size;
+    const uint64_t* pos;
+    const uint64_t* end;
+    const int32_t* err;        // optional
+    const uint32_t* n_frames;  // device count ...
+    uint32_t n_frames_host;    // ... or host count when n_frames == nullptr
+    uint32_t cap;
+    uint32_t* bad;             // per frame: 1 when the stored CRC-16 differs
 };
 
 }  // namespace zflac

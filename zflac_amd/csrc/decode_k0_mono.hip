@@ -3,7 +3,9 @@
 #include "decode.inc"
 
 namespace zflac {
+hipError_t launch_decode_k0_mono_mix(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);  // decode_k0_mono_mix.hip
 hipError_t launch_decode_k0_mono(const DecodeArgs& a, uint32_t max_frames, hipStream_t st) {
-    return launch_decode_layout<0, LAY_MONO>(a, max_frames, st);
+    const hipError_t e = launch_decode_layout<0, LAY_MONO>(a, max_frames, st);
+    return e != hipSuccess ? e : launch_decode_k0_mono_mix(a, max_frames, st);
 }
 }  // namespace zflac

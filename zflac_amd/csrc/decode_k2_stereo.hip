@@ -3,8 +3,10 @@
 #include "decode.inc"
 
 namespace zflac {
+hipError_t launch_decode_k2_stereo_mix(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);  // decode_k2_stereo_mix.hip
 hipError_t launch_decode_k2_stereo(const DecodeArgs& a, uint32_t max_frames, hipStream_t st) {
-    return launch_decode_layout<2, LAY_STEREO>(a, max_frames, st);
+    const hipError_t e = launch_decode_layout<2, LAY_STEREO>(a, max_frames, st);
+    return e != hipSuccess ? e : launch_decode_k2_stereo_mix(a, max_frames, st);
 }
 // k_walk for this container: used by the stereo and the 3..8-channel layouts
 hipError_t launch_walk_k2(const DecodeArgs& a, uint32_t max_frames, hipStream_t st) {

@@ -66,6 +66,7 @@ static hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_fram
     return launch_decode_k2_multi(a, max_frames, st);
 }
 hipError_t launch_verify(const VerifyArgs& a, uint32_t max_items, hipStream_t st);
+hipError_t launch_crc16(const Crc16Args& a, uint32_t max_frames, hipStream_t st);
 hipError_t launch_md5(const Md5Job* jobs, uint32_t n_jobs, uint32_t* digests, hipStream_t st);
 
 namespace {
@@ -277,6 +278,7 @@ struct Class {
     DevBuf<uint64_t> c_pos, c_out, c_end;
     DevBuf<uint32_t> c_stream, c_info, c_rate, sub, group_mb;
     DevBuf<int32_t> c_err;
+    DevBuf<uint32_t> crc_bad;  // k_crc16 verdict per candidate (ZFLAC_FLAG_CHECK_CRC16)
     DevBuf<uint8_t> dummy;  // sink of masked-off packed stores (64 lanes x 32 B)
     // pinned host mirror, so the per-run read-backs are plain DMA on the batch stream:
     // [0] n_frames, [1] overflow, [2..3] unused, then one status word per member
@@ -618,7 +620,7 @@ struct SeqRunner {
     DevBuf<uint64_t> p_pos, p_out, p_end;
     DevBuf<uint32_t> p_stream, p_info, p_rate;
     DevBuf<int32_t> p_err;
-    DevBuf<uint32_t> p_sub, p_mb;
+    DevBuf<uint32_t> p_sub, p_mb, p_crc;
     DevBuf<StreamDesc> p_desc;
 
     SeqRunner(zflac_batch* b_, Class& C_, uint32_t slot_) : b(b_), C(C_), slot(slot_) {}
@@ -677,6 +679,32 @@ struct SeqRunner {
         recs.resize(n);
         for (size_t i = 0; i < n; i++) recs[i] = FrameRec{e[i], er[i], in[i], ra[i]};
     }
+
+    // k_crc16 over the frames [pos[i], end[i]); true when every trailer matches
+    bool crc16_ok(const std::vector<uint64_t>& pos, const std::vector<uint64_t>& end) {
+        const size_t n = pos.size();
+        if (!n) return true;
+        hipStream_t st = b->stream;
+        p_pos.alloc(n);
+        p_end.alloc(n);
+        p_crc.alloc(n);
+        ck(hipMemcpyAsync(p_pos.p, pos.data(), n * 8, hipMemcpyHostToDevice, st));
+        ck(hipMemcpyAsync(p_end.p, end.data(), n * 8, hipMemcpyHostToDevice, st));
+        Crc16Args a;
+        std::memset(&a, 0, sizeof(a));
+        a.in = C.in.p;
+        a.in_size = C.in.n;
+        a.pos = p_pos.p;
+        a.end = p_end.p;
+        a.n_frames_host = (uint32_t)n;
+        a.cap = (uint32_t)n;
+        a.bad = p_crc.p;
+        ck(launch_crc16(a, (uint32_t)n, st));
+        std::vector<uint32_t> bad(n);
+        ck(hipMemcpyAsync(bad.data(), p_crc.p, n * 4, hipMemcpyDeviceToHost, st));
+        ck(hipStreamSynchronize(st));
+        return std::none_of(bad.begin(), bad.end(), [](uint32_t x) { return x != 0; });
+    }
 };
 
 void finish_stream_sequential(zflac_batch* b, Class& C, uint32_t slot, const std::vector<uint32_t>& h_chunk_off,
@@ -718,7 +746,7 @@ void finish_stream_sequential(zflac_batch* b, Class& C, uint32_t slot, const std
     bool first = true;
     uint32_t rate0 = 0, count0 = 0, dcode0 = 0;
     int bps0 = 0;
-    std::vector<uint64_t> list_pos, list_out;
+    std::vector<uint64_t> list_pos, list_out, list_end;
     int err = 0;
     for (;;) {
         if (valid_total && offset >= total) break;  // :341
@@ -759,9 +787,13 @@ void finish_stream_sequential(zflac_batch* b, Class& C, uint32_t slot, const std
         if (rec.err) { err = rec.err; break; }
         list_pos.push_back(p);
         list_out.push_back(offset);
+        list_end.push_back(rec.end);
         offset += (uint64_t)bs * count0;
         p = rec.end;
     }
+    // optional CRC-16 of the frames read before the loop stopped: zflac would read each
+    // trailer before the next frame, so a mismatch there comes before `err`
+    if ((b->flags & ZFLAC_FLAG_CHECK_CRC16) && !R.crc16_ok(list_pos, list_end)) err = E_FRAME_CRC;
     s.err = err;
     if (err) return;
     // final decode of the certified chain into this stream's region (or an override)
@@ -807,6 +839,33 @@ void run_batch(zflac_batch* b) {
             C.cap = std::max<uint32_t>(C.h_misc[0] + 1024, C.cap * 2);  // candidate table overflow: grow, redo
         }
     }
+    const bool crc = (b->flags & ZFLAC_FLAG_CHECK_CRC16) != 0;
+    b->timings.crc16_ms = 0;
+    if (crc && !b->classes.empty()) {  // every candidate's trailer, after the chain checks
+        if (timing) ck(hipEventRecord(b->ev[5], b->stream));
+        for (auto& cp : b->classes) {
+            Class& C = *cp;
+            C.crc_bad.alloc(C.cap);
+            Crc16Args a;
+            std::memset(&a, 0, sizeof(a));
+            a.in = C.in.p;
+            a.in_size = C.in.n;
+            a.pos = C.c_pos.p;
+            a.end = C.c_end.p;
+            a.err = C.c_err.p;
+            a.n_frames = C.misc.p;
+            a.cap = C.cap;
+            a.bad = C.crc_bad.p;
+            ck(launch_crc16(a, std::min(C.h_misc[0], C.cap), b->stream));
+        }
+        if (timing) ck(hipEventRecord(b->ev[6], b->stream));
+        ck(hipStreamSynchronize(b->stream));
+        if (timing) {
+            float tc = 0;
+            ck(hipEventElapsedTime(&tc, b->ev[5], b->ev[6]));
+            b->timings.crc16_ms = tc;
+        }
+    }
     if (timing && !b->classes.empty()) {
         float t01 = 0, t14 = 0, t42 = 0, t23 = 0, t03 = 0;
         ck(hipEventElapsedTime(&t01, b->ev[0], b->ev[1]));
@@ -826,7 +885,12 @@ void run_batch(zflac_batch* b) {
     for (auto& cp : b->classes) {
         Class& C = *cp;
         const int esz = esz_of_kind(C.kind);
-        std::vector<uint32_t> h_off;
+        std::vector<uint32_t> h_off, h_crc;
+        const uint32_t nfr = std::min(C.h_misc[0], C.cap);
+        if (crc && nfr) {
+            h_crc.resize(nfr);
+            ck(hipMemcpy(h_crc.data(), C.crc_bad.p, nfr * 4, hipMemcpyDeviceToHost));
+        }
         for (size_t m = 0; m < C.members.size(); m++) {
             StreamState& s = b->streams[C.members[m]];
             s.override_out.reset();
@@ -840,6 +904,20 @@ void run_batch(zflac_batch* b) {
                 s.info.channels = (uint8_t)s.nch;
                 s.info.sample_rate = s.first.rate;
                 s.info.bits_per_sample = (uint8_t)depth_bits_h(s.first.dcode, (int)s.si.bps);
+                if (crc) {  // a certified stream's candidates are exactly its frames
+                    if (h_off.empty()) {
+                        h_off.resize(C.chunks.size() + 1);
+                        ck(hipMemcpy(h_off.data(), C.chunk_off.p, h_off.size() * 4, hipMemcpyDeviceToHost));
+                    }
+                    const uint32_t f0 = std::min(h_off[D.first_chunk], nfr), f1 = std::min(h_off[D.end_chunk], nfr);
+                    for (uint32_t f = f0; f < f1; f++)
+                        if (h_crc[f]) {
+                            s.err = E_FRAME_CRC;
+                            s.info = zflac_info{};
+                            s.info.sample_kind = (uint8_t)C.kind;
+                            break;
+                        }
+                }
             } else {
                 if (h_off.empty()) {
                     h_off.resize(C.chunks.size() + 1);
@@ -1113,6 +1191,7 @@ const char* zflac_hip_error_name(int code) {
         case 13: return "DeviceError";
         case 14: return "InvalidArgument";
         case 15: return "OutOfDomain";
+        case 16: return "FrameCrcMismatch";
         default: return "Unknown";
     }
 }
@@ -1207,9 +1286,14 @@ void zflac_hip_batch_destroy(zflac_batch* b) {
 }
 
 int zflac_hip_open(const uint8_t* buf, size_t len, int device, zflac_batch** out_batch, zflac_info* info) {
+    return zflac_hip_open_ex(buf, len, device, 0, out_batch, info);
+}
+
+int zflac_hip_open_ex(const uint8_t* buf, size_t len, int device, int flags, zflac_batch** out_batch,
+                      zflac_info* info) {
     if (!out_batch) return E_INVALID_ARGUMENT;
     zflac_stream s{buf, len};
-    int rc = create_batch(&s, 1, device, 0, out_batch);
+    int rc = create_batch(&s, 1, device, flags, out_batch);
     if (rc) return rc;
     rc = zflac_hip_batch_run(*out_batch);
     if (rc) return rc;

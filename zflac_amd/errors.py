@@ -9,6 +9,7 @@ NAMES = {
     5: "InvalidChecksum", 6: "InvalidFrameHeader", 7: "InconsistentParameters", 8: "InvalidCodedNumber",
     9: "InvalidSubframeHeader", 10: "InvalidResidualCodingMethod", 11: "EndOfStream", 12: "OutOfMemory",
     13: "DeviceError", 14: "InvalidArgument", 15: "OutOfDomain",
+    16: "FrameCrcMismatch",  # only with the opt-in CRC-16 check (zflac ignores the trailer)
 }
 
 
