@@ -73,7 +73,13 @@ struct FrameHdr {
     bool crc_ok;
 };
 
-__device__ __forceinline__ FrameHdr parse_frame_header(const uint8_t* p, uint64_t avail, uint32_t si_rate) {
+// `at(i)` returns header byte i (global memory, or an LDS copy in k_scan); CRC = false skips
+// the CRC-8 (the decode kernels only need the fields: candidates were filtered already).
+// `crc_tab` is the CRC-8 table (an LDS copy in k_scan: a per-lane table lookup in constant
+// memory is a global-latency load per byte).
+template <bool CRC, typename At>
+__device__ __forceinline__ FrameHdr parse_frame_header_t(At&& at, uint64_t avail, uint32_t si_rate,
+                                                         const uint8_t* crc_tab) {
     FrameHdr h;
     h.bs = h.rate = h.hdr_len = 0;
     h.chan_code = h.dcode = h.byte1 = h.zero_bit = h.bs_code = 0;
@@ -81,7 +87,7 @@ __device__ __forceinline__ FrameHdr parse_frame_header(const uint8_t* p, uint64_
     h.crc_eof = false;
     h.crc_ok = false;
     if (avail < 4) { h.err = E_END_OF_STREAM; return h; }
-    const uint32_t b0 = p[0], b1 = p[1], b2 = p[2], b3 = p[3];
+    const uint32_t b0 = at(0), b1 = at(1), b2 = at(2), b3 = at(3);
     h.byte1 = b1;
     h.chan_code = b3 >> 4;
     h.dcode = (b3 >> 1) & 7;
@@ -91,7 +97,7 @@ __device__ __forceinline__ FrameHdr parse_frame_header(const uint8_t* p, uint64_
     uint32_t idx = 4;
     // read_coded_number (:203-214)
     if (avail <= idx) { h.err = E_END_OF_STREAM; return h; }
-    const uint32_t first = p[idx++];
+    const uint32_t first = at(idx++);
     const uint32_t ones = __clz((~first & 0xFFu) << 24) > 8 ? 8 : __clz((~first & 0xFFu) << 24);
     if (first == 0xFF || ones == 1) { h.err = E_INVALID_CODED_NUMBER; return h; }
     if (ones >= 2) {
@@ -103,10 +109,10 @@ __device__ __forceinline__ FrameHdr parse_frame_header(const uint8_t* p, uint64_
     if (bc == 0) { h.err = E_INVALID_FRAME_HEADER; return h; }
     if (bc == 6) {
         if (avail <= idx) { h.err = E_END_OF_STREAM; return h; }
-        h.bs = (uint32_t)p[idx++] + 1;
+        h.bs = (uint32_t)at(idx++) + 1;
     } else if (bc == 7) {
         if (avail < (uint64_t)idx + 2) { h.err = E_END_OF_STREAM; return h; }
-        const uint32_t v = ((uint32_t)p[idx] << 8) | p[idx + 1];
+        const uint32_t v = ((uint32_t)at(idx) << 8) | at(idx + 1);
         idx += 2;
         if (v == 0xFFFF) { h.err = E_INVALID_FRAME_HEADER; return h; }
         h.bs = v + 1;
@@ -123,10 +129,10 @@ __device__ __forceinline__ FrameHdr parse_frame_header(const uint8_t* p, uint64_
         h.rate = si_rate;
     } else if (rc == 12) {
         if (avail <= idx) { h.err = E_END_OF_STREAM; return h; }
-        h.rate = p[idx++];
+        h.rate = at(idx++);
     } else if (rc == 13 || rc == 14) {
         if (avail < (uint64_t)idx + 2) { h.err = E_END_OF_STREAM; return h; }
-        h.rate = ((uint32_t)p[idx] << 8) | p[idx + 1];
+        h.rate = ((uint32_t)at(idx) << 8) | at(idx + 1);
         if (rc == 14) h.rate *= 10;
         idx += 2;
     } else if (rc == 15) {
@@ -142,11 +148,22 @@ __device__ __forceinline__ FrameHdr parse_frame_header(const uint8_t* p, uint64_
         h.crc_eof = true;
         return h;
     }
-    uint32_t crc = 0;
-    for (uint32_t i = 0; i < idx; i++) crc = CRC8.t[crc ^ p[i]];
-    h.crc_ok = crc == p[idx];
+    if constexpr (CRC) {
+        uint32_t crc = 0;
+        for (uint32_t i = 0; i < idx; i++) crc = crc_tab[crc ^ at(i)];
+        h.crc_ok = crc == at(idx);
+    }
     return h;
 }
+
+__device__ __forceinline__ FrameHdr parse_frame_header(const uint8_t* p, uint64_t avail, uint32_t si_rate) {
+    return parse_frame_header_t<true>([p](uint32_t i) -> uint32_t { return p[i]; }, avail, si_rate, CRC8.t);
+}
+__device__ __forceinline__ FrameHdr parse_frame_fields(const uint8_t* p, uint64_t avail, uint32_t si_rate) {
+    return parse_frame_header_t<false>([p](uint32_t i) -> uint32_t { return p[i]; }, avail, si_rate, nullptr);
+}
+
+
 
 // Filter for sync candidates: a well-formed header consistent with the stream's first
 // frame. Anything it rejects that zflac would still decode breaks the verified chain and
