@@ -193,3 +193,16 @@ def tile_flac(st: Stream, reps: int, unknown_total: bool = False) -> bytes:
         h.update(msg)
     d[o + 18:o + 34] = h.digest()
     return bytes(d) + st.flac[st.frames_begin:] * reps
+
+
+def header_crc8_index(flac: bytes, off: int) -> int:
+    """Offset of the CRC-8 byte of the frame header at `off` (src/zflac.zig:343-407 layout:
+    sync + 2 bytes, UTF-8-style coded number, uncommon block size / rate bytes)."""
+    b2, first = flac[off + 2], flac[off + 4]
+    ones = 0
+    while ones < 8 and first & (0x80 >> ones):
+        ones += 1
+    idx = 5 + (ones - 1 if ones >= 2 else 0)
+    idx += {6: 1, 7: 2}.get(b2 >> 4, 0)
+    idx += {12: 1, 13: 2, 14: 2}.get(b2 & 15, 0)
+    return off + idx

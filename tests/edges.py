@@ -110,6 +110,18 @@ def incorrect_metadata_length_case(flac: bytes, frames_begin: int) -> bytes:
     return b"fLaC" + bytes(si) + pad_bad + pad_last + flac[frames_begin:]
 
 
+def bad_crc8_case(frames: int = 48, seed: int = 95, write_total: int = 1):
+    """Every frame header's CRC-8 byte flipped. zflac never checks it (:407-410), so the
+    stream decodes to the source PCM; the device indexer drops every header and the
+    sequential planner reaches each frame through its batched probes."""
+    st = synth.generate(**dict(STEREO16, stereo_mode=10, n_samples=4096 * frames, seed=seed,
+                               write_total=write_total))
+    b = bytearray(st.flac)
+    for off in st.frame_offsets:
+        b[synth.header_crc8_index(st.flac, int(off))] ^= 0x5A
+    return bytes(b), st.pcm
+
+
 def fixture_mutants(n_per_file: int = 100, seed: int = 0x0F1A):
     """Seeded bit-flip mutants of the committed C3 / C4 fixtures. Flips land in the frame
     section (90 %) or in the metadata outside the 36-bit total-samples field (whose huge

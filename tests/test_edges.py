@@ -163,6 +163,27 @@ def test_gpu_planted_sync_repair(gpu_ready):
     b.close()
 
 
+def test_bad_crc8_case_on_the_oracle():
+    data, pcm = edges.bad_crc8_case(frames=6)
+    r = oracle.decode(data)
+    assert r.error == "OK"
+    np.testing.assert_array_equal(r.samples, pcm.reshape(-1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("total", [1, 0])
+def test_gpu_bad_crc8_headers_batched_probes(gpu_ready, total):
+    """No header passes the indexer's CRC-8 filter: the sequential planner gets every record
+    from its batched probes (a handful of launches, not one per frame)."""
+    data, pcm = edges.bad_crc8_case(frames=300, write_total=total)
+    t0 = time.perf_counter()
+    d = zflac_amd.decode(data)
+    dt = time.perf_counter() - t0
+    np.testing.assert_array_equal(d.samples.values, pcm.reshape(-1))
+    print(f"300 frames, every CRC-8 wrong: decode() {dt * 1e3:.1f} ms")
+    assert dt < 10.0
+
+
 @pytest.mark.gpu
 def test_gpu_faulty11(gpu_ready):
     st = synth.generate(**edges.STEREO16)

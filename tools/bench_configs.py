@@ -31,7 +31,8 @@ import zflac_amd  # noqa: E402
 
 B = 4096
 ROWS = {
-    # name: (flacgen config of one segment, segment frames, total frames, unknown total)
+    # name: (flacgen config of one segment, segment frames, total frames, unknown total or
+    # "bad_crc8")
     "C2 mono 16-bit fixed-2 k=4": (synth.config_c2(), 1024, 65536, False),
     "C3 stereo M/S 16-bit LPC-8": (synth.config_c3(), 1024, 65536, False),
     "C4 stereo 24-bit LPC-32 shift 15 wasted 4": (synth.config_c4(), 512, 65536, False),
@@ -51,13 +52,22 @@ ROWS = {
     "C3, total unknown (sequential planner)": (synth.config_c3(), 256, 4096, True),
     "C3, planted false syncs (repair path)": (dict(channels=2, bps=16, stereo_mode=1, order=8, block_size=B,
                                                    plant_sync_every=2), 256, 4096, False),
+    # every header's CRC-8 byte wrong (zflac ignores it): the indexer drops every header and
+    # the sequential planner finds the frames through its batched probes
+    "C3, every header CRC-8 wrong (batched probes)": (synth.config_c3(), 4096, 4096, "bad_crc8"),
 }
 
 
 def run_row(name, cfg, seg, frames, unknown, steps):
     st = synth.generate(**dict(cfg, n_samples=B * seg, seed=cfg.get("seed", 7)))
     reps = max(1, frames // seg)
-    data = synth.tile_flac(st, reps, unknown_total=unknown)
+    if unknown == "bad_crc8":  # one generated stream, every header CRC-8 flipped
+        b = bytearray(st.flac)
+        for off in st.frame_offsets:
+            b[synth.header_crc8_index(st.flac, int(off))] ^= 0x5A
+        data, reps = bytes(b), 1
+    else:
+        data = synth.tile_flac(st, reps, unknown_total=unknown)
     n = st.pcm.size * reps
     # device-resident batch runs
     b = zflac_amd.Batch([data], timing=True)

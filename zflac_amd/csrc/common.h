@@ -157,6 +157,20 @@ struct VerifyArgs {
     uint32_t* status;           // per stream: nonzero => take the sequential path
 };
 
+// k_sync_list (scan.hip): sync codes in [lo, hi) with a parseable header matching the
+// stream's first frame (channels, depth code, rate), for the sequential planner.
+struct SyncListArgs {
+    const uint8_t* in;
+    uint64_t lo, hi;       // absolute byte range to search
+    uint64_t in_end;       // end of the stream's bytes
+    uint32_t si_rate;      // STREAMINFO rate (rate code 0)
+    uint32_t rate_hz;      // the first frame's rate
+    uint32_t nch, dcode;   // the first frame's channel count and depth code
+    uint64_t* pos;         // out: positions (unordered)
+    uint32_t* count;       // out: number found (may exceed cap)
+    uint32_t cap;
+};
+
 // k_crc16 (crc16.hip): frame f covers bytes [pos[f], end[f] - 2) with its CRC-16 trailer at
 // end[f] - 2 (c_end as k_decode records it). Frames with err[f] != 0 are skipped.
 struct Crc16Args {

@@ -67,6 +67,7 @@ static hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_fram
 }
 hipError_t launch_verify(const VerifyArgs& a, uint32_t max_items, hipStream_t st);
 hipError_t launch_crc16(const Crc16Args& a, uint32_t max_frames, hipStream_t st);
+hipError_t launch_sync_list(const SyncListArgs& a, hipStream_t st);
 hipError_t launch_md5(const Md5Job* jobs, uint32_t n_jobs, uint32_t* digests, hipStream_t st);
 
 namespace {
@@ -620,7 +621,8 @@ struct SeqRunner {
     DevBuf<uint64_t> p_pos, p_out, p_end;
     DevBuf<uint32_t> p_stream, p_info, p_rate;
     DevBuf<int32_t> p_err;
-    DevBuf<uint32_t> p_sub, p_mb, p_crc;
+    DevBuf<uint32_t> p_sub, p_mb, p_crc, p_cnt;
+    DevBuf<uint64_t> p_sync;
     DevBuf<StreamDesc> p_desc;
 
     SeqRunner(zflac_batch* b_, Class& C_, uint32_t slot_) : b(b_), C(C_), slot(slot_) {}
@@ -678,6 +680,41 @@ struct SeqRunner {
         ck(hipStreamSynchronize(st));
         recs.resize(n);
         for (size_t i = 0; i < n; i++) recs[i] = FrameRec{e[i], er[i], in[i], ra[i]};
+    }
+
+    // Sync codes in [lo, hi) whose header matches the stream (k_sync_list), sorted.
+    std::vector<uint64_t> sync_list(uint64_t lo, uint64_t hi, const StreamDesc& D) {
+        hipStream_t st = b->stream;
+        uint32_t cap = 4096, n = 0;
+        for (int attempt = 0; attempt < 2; attempt++) {
+            p_sync.alloc(cap);
+            p_cnt.alloc(1);
+            ck(hipMemsetAsync(p_cnt.p, 0, 4, st));
+            SyncListArgs a;
+            a.in = C.in.p;
+            a.lo = lo;
+            a.hi = hi;
+            a.in_end = D.in_end;
+            a.si_rate = D.si_rate;
+            a.rate_hz = D.rate_hz;
+            a.nch = D.nch;
+            a.dcode = D.dcode;
+            a.pos = p_sync.p;
+            a.count = p_cnt.p;
+            a.cap = cap;
+            ck(launch_sync_list(a, st));
+            ck(hipMemcpyAsync(&n, p_cnt.p, 4, hipMemcpyDeviceToHost, st));
+            ck(hipStreamSynchronize(st));
+            if (n <= cap) break;
+            cap = n;  // more than fit: once more with room for all
+        }
+        std::vector<uint64_t> out(std::min(n, cap));
+        if (!out.empty()) {
+            ck(hipMemcpyAsync(out.data(), p_sync.p, out.size() * 8, hipMemcpyDeviceToHost, st));
+            ck(hipStreamSynchronize(st));
+        }
+        std::sort(out.begin(), out.end());
+        return out;
     }
 
     // k_crc16 over the frames [pos[i], end[i]); true when every trailer matches
@@ -748,6 +785,9 @@ void finish_stream_sequential(zflac_batch* b, Class& C, uint32_t slot, const std
     int bps0 = 0;
     std::vector<uint64_t> list_pos, list_out, list_end;
     int err = 0;
+    // batched probes: a chain position without a record asks for every matching sync code
+    // in a window ahead of it (doubling, 1 .. 64 MiB) and decodes them in one launch
+    uint64_t probe_win = 1ull << 20;
     for (;;) {
         if (valid_total && offset >= total) break;  // :341
         if (D.in_end - p < 4) {                     // :343-350
@@ -759,9 +799,14 @@ void finish_stream_sequential(zflac_batch* b, Class& C, uint32_t slot, const std
         if (it != recs.end()) {
             rec = it->second;
         } else {
-            std::vector<FrameRec> one;
-            R.run_list({p}, {0}, probe_desc, C.out.p, 0, one);
-            rec = one[0];
+            const uint64_t hi = std::min<uint64_t>(D.in_end, p + probe_win);
+            probe_win = std::min<uint64_t>(probe_win * 2, 64ull << 20);
+            std::vector<uint64_t> pos = R.sync_list(p, hi, D);
+            if (pos.empty() || pos[0] != p) pos.insert(pos.begin(), p);  // zflac reads p whatever it holds
+            std::vector<FrameRec> got;
+            R.run_list(pos, std::vector<uint64_t>(pos.size(), 0), probe_desc, C.out.p, 0, got);
+            for (size_t i = 0; i < pos.size(); i++) recs[pos[i]] = got[i];
+            rec = recs[p];
         }
         if (rec.info & INFO_PRE_ERR) { err = rec.err; break; }
         const uint32_t bs = (rec.info & 0xFFFF) + 1, code = (rec.info >> 16) & 15, dcode = (rec.info >> 20) & 7;

@@ -283,6 +283,28 @@ __global__ void k_verify(VerifyArgs a) {
 }
 
 // ----------------------------------------------------------------------------------
+// k_sync_list: the sequential planner's batched probes. Every frame sync code in [lo, hi)
+// whose header parses and matches the stream's channels, depth and rate: what zflac's
+// frame loop checks (:343-392), without the fast path's CRC-8, reserved-bit and
+// blocking-byte filters. Unordered (the host sorts).
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(SCAN_THREADS) void k_sync_list(SyncListArgs a) {
+    const uint64_t abase = a.lo & ~(uint64_t)15;
+    const uint64_t nwin = (a.hi - abase + 15) / 16;
+    for (uint64_t w = (uint64_t)blockIdx.x * SCAN_THREADS + threadIdx.x; w < nwin;
+         w += (uint64_t)gridDim.x * SCAN_THREADS) {
+        scan_window(a.in, abase + w * 16, a.lo, a.hi, [&](uint64_t p) {
+            const FrameHdr h = parse_frame_header(a.in + p, a.in_end - p, a.si_rate);
+            if (h.err || h.crc_eof || channels_count(h.chan_code) != a.nch || h.dcode != a.dcode ||
+                h.rate != a.rate_hz)
+                return;
+            const uint32_t slot = atomicAdd(a.count, 1u);
+            if (slot < a.cap) a.pos[slot] = p;
+        });
+    }
+}
+
+// ----------------------------------------------------------------------------------
 // launchers
 // ----------------------------------------------------------------------------------
 hipError_t launch_scan(const ScanArgs& a, hipStream_t st) {
@@ -298,6 +320,14 @@ hipError_t launch_scan_chunks(const uint32_t* cnt, const unsigned long long* uni
 hipError_t launch_compact(const CompactArgs& a, hipStream_t st) {
     if (a.n_chunks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_compact, dim3(a.n_chunks), dim3(SCAN_THREADS), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_sync_list(const SyncListArgs& a, hipStream_t st) {
+    if (a.hi <= a.lo) return hipSuccess;
+    const uint64_t windows = (a.hi - (a.lo & ~(uint64_t)15) + 15) / 16;
+    uint64_t blocks = (windows + SCAN_THREADS - 1) / SCAN_THREADS;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_sync_list, dim3((uint32_t)blocks), dim3(SCAN_THREADS), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_verify(const VerifyArgs& a, uint32_t max_items, hipStream_t st) {
