@@ -3,10 +3,13 @@ decode() measured end to end.
 
 Workload (BASELINE.json configs[4], per-GPU share; its codec parameters are configs[2]):
 1250 independent stereo 16-bit mid/side streams per GPU, 32 frames x 4096 samples each,
-LPC order 8 (synthetic, seeded per global stream index). One "step" = one call of
-zflac_hip_batch_run over the rank's whole shard: frame-sync scan, candidate compaction,
-subframe decode (Rice, LPC rollback, decorrelation, PCM pack-out) and chain verification,
-inputs already in HBM, outputs left in HBM. N GPUs = N ranks with disjoint shards (weak
+LPC order 8 (synthetic, seeded per global stream index). One "step" = one batch run
+(zflac_hip_batch_submit + _wait) over the rank's whole shard: frame-sync scan, candidate
+compaction, subframe decode (Rice, LPC rollback, decorrelation, PCM pack-out) and chain
+verification, inputs already in HBM, outputs left in HBM. Two runs are kept in flight
+(--inflight 2, each with its own buffers and HIP stream), so one step's scan and walk
+overlap the previous step's decode; `ms_per_step_serial` is the same shard one run at a
+time. N GPUs = N ranks with disjoint shards (weak
 scaling, no collective in the data path; torch.distributed only for the timing barrier
 and the max over ranks).
 
@@ -73,6 +76,7 @@ def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None, help="ranks (one per GPU); default WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--inflight", type=int, default=2, help="shard runs overlapped on the device (1 = serial)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--streams-per-gpu", type=int, default=STREAMS_PER_GPU)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample budget (all cores)")
@@ -324,26 +328,62 @@ def main():
 
     import zflac_amd
 
-    batch = zflac_amd.Batch(streams, device=device, timing=True)
-    for _ in range(args.warmup):
-        batch.run()
-    barrier_sync()
-    t0 = time.perf_counter()
+    # `inflight` runs of the shard overlap on the device: each has its own Batch (HIP stream,
+    # input copy, candidate tables, output), and step k+1 is submitted before step k is
+    # waited for, so one run's scan and walk execute beside the other's decode. Every step
+    # still decodes and verifies the whole shard.
+    n_inf = max(1, args.inflight)
+    batches = [zflac_amd.Batch(streams, device=device, timing=True) for _ in range(n_inf)]
     dec_ms, walk_ms, scan_ms, ver_ms = [], [], [], []
-    for _ in range(args.steps):
-        batch.run()
-        t = batch.timings()
+
+    def record(b):
+        t = b.timings()
         dec_ms.append(t.decode_ms)
         walk_ms.append(t.walk_ms)
         scan_ms.append(t.scan_ms)
         ver_ms.append(t.verify_ms)
+
+    def run_steps(k, bs, rec):
+        pending = [False] * len(bs)
+        for i in range(k):
+            j = i % len(bs)
+            if pending[j]:
+                bs[j].wait()
+                if rec:
+                    record(bs[j])
+            bs[j].submit()
+            pending[j] = True
+        for t in range(len(bs)):  # drain, oldest first
+            j = (k + t) % len(bs)
+            if pending[j]:
+                bs[j].wait()
+                if rec:
+                    record(bs[j])
+
+    run_steps(args.warmup, batches, False)
+    barrier_sync()
+    t0 = time.perf_counter()
+    run_steps(args.steps, batches, True)
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    tm = batch.timings()
+    tm = batches[0].timings()
     samples_rank = tm.samples
     in_bytes, out_bytes = tm.input_bytes, tm.output_bytes
 
-    errs = [] if args.no_verify else verify(batch, streams)
+    # the same shard one run at a time (no overlap), for reference
+    serial = None
+    if n_inf > 1:
+        t1 = time.perf_counter()
+        run_steps(args.steps, batches[:1], False)
+        serial = (time.perf_counter() - t1) / args.steps
+
+    errs = []
+    if not args.no_verify:
+        for b in batches:
+            errs += verify(b, streams)
+    for b in batches[1:]:
+        b.close()
+    batch = batches[0]
     tot = aggregate(dist, coll_dev, elapsed, samples_rank, in_bytes, out_bytes, len(errs))
     elapsed = tot.elapsed_s
     samples_all, in_all, out_all = tot.samples, tot.input_bytes, tot.output_bytes
@@ -399,6 +439,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
+            "inflight": n_inf,
+            "ms_per_step_serial": round(serial * 1e3, 4) if serial else None,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

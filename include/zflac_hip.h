@@ -118,6 +118,15 @@ int zflac_hip_batch_create(const zflac_stream *streams, size_t n, int device, in
  * outputs left in HBM). Synchronous. Returns ZFLAC_OK or ZFLAC_E_DEVICE; per-stream
  * zflac errors are reported by zflac_hip_batch_info. */
 int zflac_hip_batch_run(zflac_batch *b);
+/* zflac_hip_batch_run in two halves, so that runs of different batches overlap on the
+ * device: _submit enqueues the run's kernels on the batch's own HIP stream and returns;
+ * _wait blocks until they finish and produces the per-stream results (the sequential
+ * planner, CRC-16 and MD5 legs run here). A batch has at most one run in flight: _submit
+ * on a submitted batch and _wait without one return ZFLAC_E_INVALID_ARGUMENT, and results
+ * (_info, _read, ...) are unavailable between the two. Destroying a submitted batch waits
+ * for its kernels. */
+int zflac_hip_batch_submit(zflac_batch *b);
+int zflac_hip_batch_wait(zflac_batch *b);
 /* Per-stream result of the last run: zflac error code, and shape when OK.
  * Before the first completed run: ZFLAC_E_INVALID_ARGUMENT (as for _read, _md5 and
  * _device_samples, which returns NULL). */

@@ -131,6 +131,13 @@ class Batch:
     def run(self) -> None:
         errors.check(self._L.zflac_hip_batch_run(self._h), "batch_run")
 
+    def submit(self) -> None:
+        """Enqueue a run and return (zflac_hip_batch_submit); results after wait()."""
+        errors.check(self._L.zflac_hip_batch_submit(self._h), "batch_submit")
+
+    def wait(self) -> None:
+        errors.check(self._L.zflac_hip_batch_wait(self._h), "batch_wait")
+
     def info(self, i: int):
         inf = _lib.zflac_info()
         rc = self._L.zflac_hip_batch_info(self._h, i, ctypes.byref(inf))

@@ -308,11 +308,14 @@ struct zflac_batch {
     std::vector<std::unique_ptr<zflac::Class>> classes;
     hipEvent_t ev[8] = {};
     bool have_timing = false;
-    bool ran = false;  // results exist only after a completed batch_run
+    bool ran = false;        // results exist only after a completed batch_run / batch_wait
+    bool submitted = false;  // batch_submit enqueued a run that batch_wait has not finished
+    double submit_t0 = 0;    // host clock at submit (run_wall_ms)
     zflac::DevBuf<zflac::Md5Job> md5_jobs;
     zflac::DevBuf<uint32_t> md5_dig;
     zflac_timings timings = {};
     ~zflac_batch() {
+        if (stream) (void)hipStreamSynchronize(stream);  // a submitted run may still use the buffers
         classes.clear();
         for (auto& s : streams) s.override_out.reset();
         for (auto& e : ev)
@@ -871,17 +874,34 @@ void finish_stream_sequential(zflac_batch* b, Class& C, uint32_t slot, const std
 
 void run_md5_device(zflac_batch* b, bool timing);
 
-void run_batch(zflac_batch* b) {
+// Phase 1 of a run: every class's parallel pipeline on the batch's stream, no host wait.
+// Two batches submitted back to back overlap on the device (each has its own stream and
+// buffers): the scan and walk of one run beside the decode of the other.
+void submit_batch(zflac_batch* b) {
     ck(hipSetDevice(b->device));
     const bool timing = (b->flags & ZFLAC_FLAG_TIMING) != 0;
     for (size_t ci = 0; ci < b->classes.size(); ci++) {
         Class& C = *b->classes[ci];
+        alloc_candidates(C);
+        enqueue_class(b, C, timing && ci == 0, timing && ci + 1 == b->classes.size());
+    }
+}
+
+// Phase 2: wait for the pipeline, redo a class whose candidate table overflowed (grown,
+// synchronously; not part of the recorded kernel timings), then the per-stream results,
+// the sequential planner for streams the chain check did not certify, CRC-16 and MD5.
+void finish_batch(zflac_batch* b) {
+    ck(hipSetDevice(b->device));
+    const bool timing = (b->flags & ZFLAC_FLAG_TIMING) != 0;
+    ck(hipStreamSynchronize(b->stream));
+    for (size_t ci = 0; ci < b->classes.size(); ci++) {
+        Class& C = *b->classes[ci];
         for (int attempt = 0; attempt < 3; attempt++) {
-            alloc_candidates(C);
-            enqueue_class(b, C, timing && ci == 0, timing && ci + 1 == b->classes.size());
-            ck(hipStreamSynchronize(b->stream));
             if (!C.h_misc[1] && C.h_misc[0] <= C.cap) break;
             C.cap = std::max<uint32_t>(C.h_misc[0] + 1024, C.cap * 2);  // candidate table overflow: grow, redo
+            alloc_candidates(C);
+            enqueue_class(b, C, false, false);
+            ck(hipStreamSynchronize(b->stream));
         }
     }
     const bool crc = (b->flags & ZFLAC_FLAG_CHECK_CRC16) != 0;
@@ -1253,13 +1273,31 @@ int zflac_hip_batch_create(const zflac_stream* streams, size_t n, int device, in
     return create_batch(streams, n, device, flags, out);
 }
 
-int zflac_hip_batch_run(zflac_batch* b) {
-    if (!b) return E_INVALID_ARGUMENT;
+int zflac_hip_batch_submit(zflac_batch* b) {
+    if (!b || b->submitted) return E_INVALID_ARGUMENT;
     b->ran = false;
     try {
-        const double t0 = now_ms();
-        run_batch(b);
-        b->timings.run_wall_ms = now_ms() - t0;
+        b->submit_t0 = now_ms();
+        b->submitted = true;
+        submit_batch(b);
+    } catch (const DeviceError&) {
+        (void)hipStreamSynchronize(b->stream);
+        b->submitted = false;
+        return E_DEVICE;
+    } catch (const std::bad_alloc&) {
+        (void)hipStreamSynchronize(b->stream);
+        b->submitted = false;
+        return E_OUT_OF_MEMORY;
+    }
+    return E_OK;
+}
+
+int zflac_hip_batch_wait(zflac_batch* b) {
+    if (!b || !b->submitted) return E_INVALID_ARGUMENT;
+    b->submitted = false;
+    try {
+        finish_batch(b);
+        b->timings.run_wall_ms = now_ms() - b->submit_t0;
         b->ran = true;
     } catch (const DeviceError&) {
         return E_DEVICE;
@@ -1267,6 +1305,11 @@ int zflac_hip_batch_run(zflac_batch* b) {
         return E_OUT_OF_MEMORY;
     }
     return E_OK;
+}
+
+int zflac_hip_batch_run(zflac_batch* b) {
+    const int rc = zflac_hip_batch_submit(b);
+    return rc ? rc : zflac_hip_batch_wait(b);
 }
 
 size_t zflac_hip_batch_size(zflac_batch* b) { return b ? b->streams.size() : 0; }
