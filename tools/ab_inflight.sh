@@ -1,11 +1,15 @@
 #!/bin/bash
-# Same-box A/B: walk workgroup size (2 vs 4 waves) x runs in flight (1, 2, 3), twice each.
+# Same-box A/B of library builds (ZFLAC_HIP_LIB) x shard runs in flight, twice each.
+# Usage: tools/ab_inflight.sh "<lib> <lib> ..." "<inflight> <inflight> ..." [tag]
 set -e
-mkdir -p gpurun_out/abinf
+LIBS=${1:-"zflac_amd/libzflac_hip.so"}
+NS=${2:-"1 2 3"}
+TAG=${3:-abinf}
+mkdir -p gpurun_out/$TAG
 for i in 1 2; do
-for L in zflac_amd/libzflac_hip.so tools/_build/lib_walk256.so; do
-for N in 1 2 3; do
+for L in $LIBS; do
+for N in $NS; do
   n=$(basename $L .so)
   ZFLAC_HIP_LIB=$L timeout -k 10 200 python bench.py --no-e2e --no-cpu-baseline --no-md5 --no-verify --steps 40 --inflight $N \
-    > gpurun_out/abinf/${n}_inf${N}_$i.json 2> gpurun_out/abinf/${n}_inf${N}_$i.err
+    > gpurun_out/$TAG/${n}_inf${N}_$i.json 2> gpurun_out/$TAG/${n}_inf${N}_$i.err
 done; done; done
