@@ -171,6 +171,43 @@ def test_batch_rerun_is_stable(gpu_ready):
     b.close()
 
 
+def test_overlapped_batches_submit_wait(gpu_ready):
+    """zflac_hip_batch_submit / _wait: three batches in flight at once on their own HIP
+    streams (the bench's pipelined mode), a mixed-class batch and a flagged-stream batch
+    among them; every result equals the oracle, and the usage errors hold (double submit,
+    wait without submit, results between submit and wait, destroy while in flight)."""
+    names = sorted(PARITY_CONFIGS)
+    mixed = [synth.generate(**dict(PARITY_CONFIGS[n], seed=3000 + i)).flac for i, n in enumerate(names)]
+    c5 = [s.flac for s in synth.generate_many([synth.config_c5(i) for i in range(64)])]
+    bad = [_CASES[c][0] for c in ("bad_sync_frame2", "wrong_md5", "bad_crc8_frame1")] + c5[:3]
+    groups = [c5, mixed, bad]
+    bs = [zflac_amd.Batch(g, timing=True) for g in groups]
+    for rnd in range(2):
+        for b in bs:
+            b.submit()
+        with pytest.raises(errors.InvalidArgument):
+            bs[0].submit()
+        assert bs[1].info(0)[0] == errors.InvalidArgument.code
+        for b in reversed(bs):
+            b.wait()
+        with pytest.raises(errors.InvalidArgument):
+            bs[2].wait()
+        for g, b in zip(groups, bs):
+            for i in range(0, len(g), 7 if g is c5 else 1):
+                r = oracle.decode(g[i], "fast")
+                try:
+                    d = b.read(i)
+                    err = "OK"
+                except errors.ZflacError as e:
+                    err, d = type(e).__name__, None
+                assert err == r.error, (rnd, i)
+                if d is not None:
+                    np.testing.assert_array_equal(d.samples.values, r.samples)
+    bs[0].submit()
+    for b in bs:
+        b.close()  # the in-flight one waits for its kernels first
+
+
 def test_c5_shard_md5_property(gpu_ready):
     """Full-shape C5 members (32 frames each) at a reduced stream count: every stream's
     decoded PCM must hash to its STREAMINFO MD5 (checked inside read) and a sample of
