@@ -38,17 +38,24 @@ ZFLAC_DECL_LAUNCH(1)
 ZFLAC_DECL_LAUNCH(2)
 #undef ZFLAC_DECL_LAUNCH
 // k_walk (subframe start offsets, 2+ channels) then k_decode; `mid` (optional) is recorded
-// between the two launches.
+// between the two launches. With a `front` stream the walk runs there and k_decode waits for
+// it on `st` through the event `join`.
 static hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_frames, hipStream_t st,
-                                hipEvent_t mid = nullptr) {
+                                hipEvent_t mid = nullptr, hipStream_t front = nullptr, hipEvent_t join = nullptr) {
     const int lay = a.nch == 2 ? 2 : (a.nch == 1 ? 1 : 0);
+    hipStream_t ws = front ? front : st;
     if (a.nch > 1) {
-        const hipError_t e = kind == 0 ? launch_walk_k0(a, max_frames, st)
-                                       : (kind == 1 ? launch_walk_k1(a, max_frames, st) : launch_walk_k2(a, max_frames, st));
+        const hipError_t e = kind == 0 ? launch_walk_k0(a, max_frames, ws)
+                                       : (kind == 1 ? launch_walk_k1(a, max_frames, ws) : launch_walk_k2(a, max_frames, ws));
         if (e != hipSuccess) return e;
     }
     if (mid) {
-        const hipError_t e = hipEventRecord(mid, st);
+        const hipError_t e = hipEventRecord(mid, ws);
+        if (e != hipSuccess) return e;
+    }
+    if (front) {
+        hipError_t e = hipEventRecord(join, front);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, join, 0);
         if (e != hipSuccess) return e;
     }
     if (kind == 0) {
@@ -304,6 +311,11 @@ struct zflac_batch {
     int device = 0;
     int flags = 0;
     hipStream_t stream = nullptr;
+    // ZFLAC_FRONT_PRIORITY=1: a second, highest-priority stream for the scan / compact / walk
+    // of each run, so that with several runs in flight their workgroups are dispatched ahead
+    // of another run's decode workgroups (an experiment knob; nullptr = one stream)
+    hipStream_t front = nullptr;
+    hipEvent_t front_join = nullptr;
     std::vector<zflac::StreamState> streams;
     std::vector<std::unique_ptr<zflac::Class>> classes;
     hipEvent_t ev[8] = {};
@@ -316,11 +328,14 @@ struct zflac_batch {
     zflac_timings timings = {};
     ~zflac_batch() {
         if (stream) (void)hipStreamSynchronize(stream);  // a submitted run may still use the buffers
+        if (front) (void)hipStreamSynchronize(front);
         classes.clear();
         for (auto& s : streams) s.override_out.reset();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
+        if (front) (void)hipStreamDestroy(front);
+        if (front_join) (void)hipEventDestroy(front_join);
     }
 };
 
@@ -549,7 +564,7 @@ DecodeArgs decode_args(Class& C) {
 
 // Launch the whole parallel pipeline of one class on the batch stream.
 void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last) {
-    hipStream_t st = b->stream;
+    hipStream_t st = b->front ? b->front : b->stream;  // scan, compact (and the walk) there
     const uint32_t nch = (uint32_t)C.chunks.size();
     ck(hipMemsetAsync(C.status.p, 0, C.members.size() * sizeof(uint32_t), st));
     ck(hipMemsetAsync(C.misc.p, 0, 4 * sizeof(uint32_t), st));
@@ -583,7 +598,8 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     ck(launch_compact(ca, st));
     if (timing_last) ck(hipEventRecord(b->ev[1], st));
     DecodeArgs da = decode_args(C);
-    ck(launch_decode(C.kind, da, C.cap, st, timing_last ? b->ev[4] : nullptr));
+    ck(launch_decode(C.kind, da, C.cap, b->stream, timing_last ? b->ev[4] : nullptr, b->front, b->front_join));
+    st = b->stream;  // decode, verify and the read-backs
     if (timing_last) ck(hipEventRecord(b->ev[2], st));
     VerifyArgs va;
     va.streams = C.d_desc.p;
@@ -1182,6 +1198,12 @@ int create_batch(const zflac_stream* streams, size_t n, int device, int flags, z
     try {
         ck(hipSetDevice(device));
         ck(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+        if (const char* fp = std::getenv("ZFLAC_FRONT_PRIORITY"); fp && fp[0] == '1') {
+            int least = 0, greatest = 0;
+            ck(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            ck(hipStreamCreateWithPriority(&b->front, hipStreamNonBlocking, greatest));
+            ck(hipEventCreateWithFlags(&b->front_join, hipEventDisableTiming));
+        }
         // timing-only events: no system-scope fence (cache writeback + invalidate) at each
         // record, which would otherwise slow the kernel after it
         for (auto& e : b->ev) ck(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
