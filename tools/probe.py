@@ -1,6 +1,6 @@
-"""Timing-probe run (experimental build with -DZFLAC_PROBE, exp/libzflac_hip_probe.so):
+"""Timing-probe run (experimental build with -DZFLAC_PROBE, tools/_build/lib_probe.so):
 cycles per chunk phase of k_walk and k_decode, summed over waves, for the C5 shard.
-Usage: ZFLAC_HIP_LIB=exp/libzflac_hip_probe.so python tools/probe.py [streams]"""
+Usage: ZFLAC_HIP_LIB=tools/_build/lib_probe.so python tools/probe.py [streams]"""
 import ctypes
 import json
 import os
@@ -24,11 +24,11 @@ fn(b._h, buf, 16)  # discard the warm-up run
 b.run()
 fn(b._h, buf, 16)
 t = b.timings()
-names = ["topup", "fast", "slow", "chunks", "fast_chunks", "redos"]
+names = ["topup", "fast", "slow", "chunks", "fast_chunks", "redos", "pair_chunks", "pair_redos"]
 out = {"streams": n, "walk_ms": t.walk_ms, "decode_ms": t.decode_ms}
 for k, base in (("walk", 0), ("decode", 8)):
-    v = [buf[base + i] for i in range(6)]
+    v = [buf[base + i] for i in range(8)]
     ch = max(1, v[3])
-    out[k] = {names[i]: v[i] for i in range(6)}
+    out[k] = {names[i]: v[i] for i in range(8)}
     out[k]["cycles_per_chunk"] = {names[i]: round(v[i] / ch, 1) for i in range(3)}
 print(json.dumps(out, indent=1))
