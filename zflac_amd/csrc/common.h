@@ -64,8 +64,11 @@ constexpr uint32_t INFO_PRE_ERR = 1u << 28;
 constexpr uint32_t INFO_CRC_EOF = 1u << 29;
 
 constexpr int SCAN_THREADS = 256;
-constexpr int SCAN_BYTES_PER_THREAD = 128;
-constexpr uint64_t CHUNK_BYTES = (uint64_t)SCAN_THREADS * SCAN_BYTES_PER_THREAD;  // 32 KiB
+#ifndef ZFLAC_SCAN_BPT
+#define ZFLAC_SCAN_BPT 128
+#endif
+constexpr int SCAN_BYTES_PER_THREAD = ZFLAC_SCAN_BPT;
+constexpr uint64_t CHUNK_BYTES = (uint64_t)SCAN_THREADS * SCAN_BYTES_PER_THREAD;  // 32 KiB by default
 constexpr int CHUNK_CAP = 64;           // candidates kept per chunk by the scan pass
 constexpr uint64_t INPUT_PAD = 4096;    // zero bytes after the last stream
 constexpr int MAX_CH = 8;               // FLAC channel limit; k_walk's per-frame record stride
@@ -121,7 +124,16 @@ struct DecodeArgs {
     uint32_t* sub_start;  // [frame][MAX_CH]: bit offset of subframe c >= 1 (k_walk -> k_decode)
     uint32_t* group_mb;   // [frame group of a k_decode wave]: its history bucket, written by the
                           // first bucket launch so the later launches skip other groups cheaply
+    uint32_t* bucket_used;  // optional: the first bucket launch ORs in bucket_bit() of every group
+    uint32_t skip_mask;     // host only: bucket_bit()s whose launches are skipped (0 = launch all)
 };
+
+// Bit of a k_decode launch (history bucket MB, MIX kernels) in DecodeArgs::bucket_used /
+// skip_mask: 8 -> 1, 4 -> 2, 16 -> 4, 32 -> 8, MIX 8 -> 16, MIX 32 -> 32. The order-8 launch
+// always runs (it classifies every wave).
+__host__ __device__ inline constexpr uint32_t bucket_bit(uint32_t mb, bool mix) {
+    return mix ? (mb <= 8 ? 16u : 32u) : (mb == 8 ? 1u : (mb == 4 ? 2u : (mb == 16 ? 4u : 8u)));
+}
 
 // One stream for k_md5 (md5.hip): the message is the decoded samples before left-justify,
 // rebuilt from the justified device samples (src/zflac.zig:267-280).

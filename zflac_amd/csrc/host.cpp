@@ -276,6 +276,10 @@ struct Class {
     std::vector<ChunkDesc> chunks;
     uint64_t in_bytes = 0, out_elems = 0;
     uint32_t cap = 0;
+    // decode launches the class's data never needs, learned from its last completed run
+    // (DecodeArgs::skip_mask; 0 until a run has completed): the buckets are a function of the
+    // input bytes alone, which a batch never changes
+    uint32_t skip_mask = 0;
     DevBuf<uint8_t> in;
     DevBuf<uint8_t> out;
     DevBuf<StreamDesc> d_desc;
@@ -289,7 +293,7 @@ struct Class {
     DevBuf<uint32_t> crc_bad;  // k_crc16 verdict per candidate (ZFLAC_FLAG_CHECK_CRC16)
     DevBuf<uint8_t> dummy;  // sink of masked-off packed stores (64 lanes x 32 B)
     // pinned host mirror, so the per-run read-backs are plain DMA on the batch stream:
-    // [0] n_frames, [1] overflow, [2..3] unused, then one status word per member
+    // [0] n_frames, [1] overflow, [2] decode buckets used, [3] unused, then one status word per member
     struct Pinned {
         uint32_t* p = nullptr;
         ~Pinned() {
@@ -598,6 +602,8 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     ck(launch_compact(ca, st));
     if (timing_last) ck(hipEventRecord(b->ev[1], st));
     DecodeArgs da = decode_args(C);
+    da.bucket_used = C.misc.p + 2;
+    da.skip_mask = C.skip_mask;
     ck(launch_decode(C.kind, da, C.cap, b->stream, timing_last ? b->ev[4] : nullptr, b->front, b->front_join));
     st = b->stream;  // decode, verify and the read-backs
     if (timing_last) ck(hipEventRecord(b->ev[2], st));
@@ -916,9 +922,11 @@ void finish_batch(zflac_batch* b) {
             if (!C.h_misc[1] && C.h_misc[0] <= C.cap) break;
             C.cap = std::max<uint32_t>(C.h_misc[0] + 1024, C.cap * 2);  // candidate table overflow: grow, redo
             alloc_candidates(C);
+            C.skip_mask = 0;
             enqueue_class(b, C, false, false);
             ck(hipStreamSynchronize(b->stream));
         }
+        if (!C.h_misc[1] && C.h_misc[0] <= C.cap) C.skip_mask = 0x3Fu & ~C.h_misc[2];
     }
     const bool crc = (b->flags & ZFLAC_FLAG_CHECK_CRC16) != 0;
     b->timings.crc16_ms = 0;
