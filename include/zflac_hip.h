@@ -140,8 +140,14 @@ int zflac_hip_batch_md5(zflac_batch *b, size_t i, uint8_t *digest16);
 /* Device pointer of stream i's samples (valid until the next run / destroy). */
 const void *zflac_hip_batch_device_samples(zflac_batch *b, size_t i);
 /* Timings of the last run / read. ZFLAC_OK when device timings were recorded
- * (ZFLAC_FLAG_TIMING); the host wall-clock fields are filled either way. */
+ * (ZFLAC_FLAG_TIMING); the host wall-clock fields are filled either way.
+ * _ex copies min(size, sizeof(zflac_timings)) bytes (pass sizeof *t) and zero-fills the
+ * rest of a longer struct, so callers built against another version of this header stay
+ * within their struct. The legacy entry point writes only the first-version layout
+ * (ZFLAC_TIMINGS_V1_SIZE bytes: scan_ms .. md5_ms). */
 int zflac_hip_batch_timings(zflac_batch *b, zflac_timings *t);
+int zflac_hip_batch_timings_ex(zflac_batch *b, zflac_timings *t, size_t size);
+#define ZFLAC_TIMINGS_V1_SIZE 80
 size_t zflac_hip_batch_size(zflac_batch *b);
 void zflac_hip_batch_destroy(zflac_batch *b);
 
@@ -151,7 +157,10 @@ void zflac_hip_batch_destroy(zflac_batch *b);
 /* Verify every stream's STREAMINFO MD5 on the device after each run (one lane per
  * stream: pays off for batches of many streams; a single long stream hashes faster on
  * the host, which zflac_hip_read / zflac_hip_batch_read do without this flag). A
- * mismatch makes the stream's result ZFLAC_E_INVALID_CHECKSUM (src/zflac.zig:279-280). */
+ * mismatch makes the stream's result ZFLAC_E_INVALID_CHECKSUM (src/zflac.zig:279-280).
+ * The hash of the streams a run certifies is enqueued by zflac_hip_batch_submit right
+ * behind that run's kernels (so it overlaps other batches' runs in flight); streams the
+ * sequential planner finishes are hashed by zflac_hip_batch_wait. */
 #define ZFLAC_FLAG_DEVICE_MD5 4
 /* Check every decoded frame's CRC-16 trailer on the device (k_crc16). zflac reads the
  * trailer and ignores it (src/zflac.zig:548-551), so this is off by default; with it, the
@@ -163,8 +172,12 @@ void zflac_hip_batch_destroy(zflac_batch *b);
 const char *zflac_hip_error_name(int code);
 /* Number of HIP devices visible; 0 means every decode will fail with ZFLAC_E_DEVICE. */
 int zflac_hip_device_count(void);
-/* Library build tag, e.g. "zflac_hip gfx950 r1". */
+/* Library build tag, e.g. "zflac_hip gfx950 r3". */
 const char *zflac_hip_version(void);
+/* ABI revision of this header; bumped whenever a struct or a signature changes.
+ * 3: zflac_hip_batch_timings_ex, zflac_hip_abi_version; device MD5 pipelined into submit. */
+#define ZFLAC_HIP_ABI_VERSION 3
+int zflac_hip_abi_version(void);
 
 #ifdef __cplusplus
 }

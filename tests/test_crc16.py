@@ -149,3 +149,28 @@ def test_crc16_batch_mixed():
             np.testing.assert_array_equal(b.read(i).samples.values, oracle.decode(streams[i]).samples)
     finally:
         b.close()
+
+
+@pytest.mark.gpu
+def test_crc16_frames_past_total_are_not_checked():
+    """A whole extra frame with a corrupted trailer after the STREAMINFO total (its header is
+    a CRC-8-valid sync): zflac stops reading at the total (src/zflac.zig:341), so the stream
+    decodes and, with the check, stays OK; the same on the batch path."""
+    import zflac_amd
+
+    st = synth.generate(**STEREO)
+    a, e = _frames(st)[1]
+    extra = _flip(st.flac[a:e], e - a - 1, 2)
+    data = st.flac + extra
+    ref = oracle.decode(data)
+    assert ref.error == "OK"
+    for crc in (False, True):
+        err, v = _decode(data, crc)
+        assert err == "OK", crc
+        np.testing.assert_array_equal(v, ref.samples)
+    b = zflac_amd.Batch([data, st.flac], check_crc16=True)
+    try:
+        b.run()
+        assert [b.error_name(i) for i in range(2)] == ["OK", "OK"]
+    finally:
+        b.close()

@@ -13,7 +13,7 @@ import zflac_amd
 from zflac_amd import errors
 
 from . import malformed
-from .util import GOLDEN, PARITY_CONFIGS, expected_samples, load_fixture_manifest, load_kats
+from .util import GOLDEN, PARITY_CONFIGS, expected_samples, load_fixture_manifest, load_kats, splice_frames
 
 pytestmark = pytest.mark.gpu
 
@@ -231,3 +231,62 @@ def test_large_single_stream(gpu_ready, cfg):
     err, d = _gpu(st.flac)  # decode() verifies the STREAMINFO MD5
     assert err == "OK"
     np.testing.assert_array_equal(d.samples.values, expected_samples(st))
+
+
+def _spliced_order_change():
+    """Frames 0-2 LPC order 8, frames 3-5 LPC order 32 (16-bit mid/side): the host predicts
+    the order-8 bucket from the first frame, so the order-32 frame groups run in a bucket
+    launch with the small grid (bucket_grid in decode.inc)."""
+    base = dict(channels=2, bps=16, stereo_mode=10, block_size=4096, n_samples=4096 * 6, partition_order=4)
+    a = synth.generate(**dict(base, order=8, precision=12, seed=4100))
+    b = synth.generate(**dict(base, order=32, precision=12, seed=4101))
+    return splice_frames(a, b, 3)
+
+
+def test_bucket_misprediction_still_decodes(gpu_ready):
+    data = _spliced_order_change()
+    r = oracle.decode(data)
+    assert r.error == "OK"
+    err, d = _gpu(data)
+    assert err == "OK"
+    np.testing.assert_array_equal(d.samples.values, r.samples)
+    # a batch of many such streams: 6 x 70 frames, so several frame groups per bucket
+    b = zflac_amd.Batch([data] * 70, timing=True)
+    b.run()
+    for i in range(0, 70, 9):
+        np.testing.assert_array_equal(b.read(i).samples.values, r.samples)
+    b.close()
+
+
+def test_pipelined_device_md5_overlapped(gpu_ready):
+    """ZFLAC_FLAG_DEVICE_MD5 with three batches in flight (submit / wait): the certified
+    streams' digests come from the k_md5 enqueued by submit, the sequential ones (a false
+    sync, an unknown total, a broken frame) from wait; every digest equals STREAMINFO and
+    hashlib over the oracle's samples, and a wrong STREAMINFO MD5 is InvalidChecksum."""
+    c5 = [s.flac for s in synth.generate_many([synth.config_c5(i, n_frames=6) for i in range(40)])]
+    seq = [synth.generate(**dict(PARITY_CONFIGS["c3_ms16_lpc8"], write_total=0, seed=4200)).flac,
+           _CASES["wrong_md5"][0], _CASES["bad_sync_frame2"][0]]
+    mixed = [synth.generate(**dict(PARITY_CONFIGS[n], seed=4300 + i)).flac
+             for i, n in enumerate(["c4_24bit_lpc32_wasted", "mono8_lpc3", "stereo12_ms", "ch3_16"])]
+    groups = [c5, seq + c5[:5], mixed]
+    bs = [zflac_amd.Batch(g, device_md5=True, timing=True) for g in groups]
+    refs = {}
+    for rnd in range(2):
+        for b in bs:
+            b.submit()
+        for b in bs:
+            b.wait()
+        for g, b in zip(groups, bs):
+            for i, data in enumerate(g):
+                if data not in refs:
+                    refs[data] = oracle.decode(data, "fast")
+                r = refs[data]
+                rc, _ = b.info(i)
+                assert errors.NAMES.get(rc) == r.error, (rnd, i)
+                if r.error != "OK":
+                    continue
+                assert b.md5(i) == _streaminfo_md5(data), (rnd, i)
+                assert b.md5(i) == _md5_pre_justify(r.samples, r.bits_per_sample), (rnd, i)
+        assert bs[0].timings().md5_ms > 0
+    for b in bs:
+        b.close()

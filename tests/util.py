@@ -106,3 +106,28 @@ PARITY_CONFIGS = {
     "lpc32_16bit": dict(channels=2, bps=16, stereo_mode=10, order=32, precision=12, block_size=4096,
                         n_samples=4096 * 2),
 }
+
+
+def splice_frames(a, b, k: int) -> bytes:
+    """Frames [0, k) of stream `a` then frames [k, n) of stream `b` (same shape: channels,
+    depth, block size, rate, frame count), under `a`'s metadata with the STREAMINFO MD5 of
+    the spliced PCM. zflac does not check frame numbers, so this is a valid stream whose
+    frames change predictor between the two parts."""
+    import hashlib
+
+    ao = [int(x) for x in a.frame_offsets] + [len(a.flac)]
+    bo = [int(x) for x in b.frame_offsets] + [len(b.flac)]
+    assert len(ao) == len(bo)
+    data = bytearray(a.flac[:ao[k]] + b.flac[bo[k]:])
+    bps, ch = a.config["bps"], a.config["channels"]
+    per = a.pcm.size // (len(ao) - 1)  # interleaved samples per (full) frame
+    pcm = np.concatenate([a.pcm[:k * per], b.pcm[k * per:]])
+    dt = container_dtype(bps)
+    if (bps + 7) // 8 * 8 == 24:
+        msg = np.ascontiguousarray(pcm.astype("<i4").view(np.uint8).reshape(-1, 4)[:, :3]).tobytes()
+    else:
+        msg = pcm.astype(np.dtype(dt).newbyteorder("<")).tobytes()
+    assert ch == b.config["channels"]
+    o = streaminfo_offset(bytes(data)) + 18
+    data[o:o + 16] = hashlib.md5(msg).digest()
+    return bytes(data)

@@ -52,6 +52,8 @@ SIGNATURES = {
     "zflac_hip_batch_md5": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_char_p]),
     "zflac_hip_batch_device_samples": (_P, [_P, ctypes.c_size_t]),
     "zflac_hip_batch_timings": (ctypes.c_int, [_P, ctypes.POINTER(zflac_timings)]),
+    "zflac_hip_batch_timings_ex": (ctypes.c_int, [_P, ctypes.POINTER(zflac_timings), ctypes.c_size_t]),
+    "zflac_hip_abi_version": (ctypes.c_int, []),
     "zflac_hip_batch_size": (ctypes.c_size_t, [_P]),
     "zflac_hip_batch_destroy": (None, [_P]),
     "zflac_hip_error_name": (ctypes.c_char_p, [ctypes.c_int]),

@@ -92,7 +92,7 @@ def decode(reader, device: int = 0, timings: dict | None = None, check_crc16: bo
         errors.check(rc)
         if timings is not None:
             t = _lib.zflac_timings()
-            L.zflac_hip_batch_timings(handle, ctypes.byref(t))
+            L.zflac_hip_batch_timings_ex(handle, ctypes.byref(t), ctypes.sizeof(t))
             timings.update({name: getattr(t, name) for name, _ in _lib.zflac_timings._fields_})
         return DecodedFLAC(info.channels, info.sample_rate, info.bits_per_sample,
                            Samples(_TAGS[info.sample_kind], out))
@@ -163,7 +163,7 @@ class Batch:
 
     def timings(self):
         t = _lib.zflac_timings()
-        rc = self._L.zflac_hip_batch_timings(self._h, ctypes.byref(t))
+        rc = self._L.zflac_hip_batch_timings_ex(self._h, ctypes.byref(t), ctypes.sizeof(t))
         return None if rc else t
 
     def device_samples(self, i: int) -> int:

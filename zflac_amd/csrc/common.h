@@ -125,11 +125,17 @@ struct DecodeArgs {
     uint32_t* group_mb;   // [frame group of a k_decode wave]: its history bucket, written by the
                           // first bucket launch so the later launches skip other groups cheaply
     uint32_t* bucket_used;  // optional: the first bucket launch ORs in bucket_bit() of every group
-    uint32_t skip_mask;     // host only: bucket_bit()s whose launches are skipped (0 = launch all)
+    uint32_t full_mask;     // host only: bucket_bit()s launched with a grid covering every frame
+                            // group (the buckets the host predicts from the input bytes); the
+                            // others get a small grid whose waves stride over the groups, so a
+                            // bucket the data never uses costs a near-empty launch (0 = all full)
 };
 
+// Grid (workgroups) of a k_decode bucket launch outside DecodeArgs::full_mask.
+constexpr uint32_t SPARSE_DECODE_BLOCKS = 64;
+
 // Bit of a k_decode launch (history bucket MB, MIX kernels) in DecodeArgs::bucket_used /
-// skip_mask: 8 -> 1, 4 -> 2, 16 -> 4, 32 -> 8, MIX 8 -> 16, MIX 32 -> 32. The order-8 launch
+// full_mask: 8 -> 1, 4 -> 2, 16 -> 4, 32 -> 8, MIX 8 -> 16, MIX 32 -> 32. The order-8 launch
 // always runs (it classifies every wave).
 __host__ __device__ inline constexpr uint32_t bucket_bit(uint32_t mb, bool mix) {
     return mix ? (mb <= 8 ? 16u : 32u) : (mb == 8 ? 1u : (mb == 4 ? 2u : (mb == 16 ? 4u : 8u)));
@@ -145,12 +151,14 @@ enum Md5Mode : uint32_t {
 };
 
 struct Md5Job {
-    const uint8_t* data;  // device samples of the stream
-    uint64_t n;           // samples
-    uint32_t mode;        // Md5Mode
-    uint32_t js;          // justify shift to undo
-    uint32_t width;       // message bytes per sample (1, 2, 3 or 4)
+    const uint8_t* data;     // device samples of the stream
+    uint64_t n;              // samples
+    uint32_t mode;           // Md5Mode
+    uint32_t js;             // justify shift to undo
+    uint32_t width;          // message bytes per sample (1, 2, 3 or 4)
     uint32_t pad_;
+    const uint32_t* status;  // optional: the stream's k_verify status; nonzero = not certified by
+                             // this run (the sequential planner decodes it later), no hash
 };
 
 struct VerifyArgs {
@@ -191,6 +199,11 @@ struct Crc16Args {
     const uint64_t* pos;
     const uint64_t* end;
     const int32_t* err;        // optional
+    // optional (the parallel pass): candidates at or past their stream's STREAMINFO total are
+    // not checked (zflac stops reading there, src/zflac.zig:341)
+    const StreamDesc* streams;
+    const uint32_t* c_stream;
+    const uint64_t* c_out;
     const uint32_t* n_frames;  // device count ...
     uint32_t n_frames_host;    // ... or host count when n_frames == nullptr
     uint32_t cap;

@@ -76,8 +76,15 @@ __global__ __launch_bounds__(CRC_THREADS) void k_crc16(Crc16Args a) {
     const uint32_t* in32 = reinterpret_cast<const uint32_t*>(a.in);
     for (uint32_t f = wave; f < n; f += nwaves) {
         const uint64_t pos = a.pos[f], end = a.end[f];
-        // frames that failed to decode have no trailer to check (their error stands)
-        const bool ok = (!a.err || a.err[f] == 0) && end >= pos + 3 && end <= a.in_size;
+        // frames that failed to decode have no trailer to check (their error stands), and
+        // candidates at or past their stream's STREAMINFO total are never read by zflac
+        // (src/zflac.zig:341): false syncs in the last frame or trailing bytes, extra frames
+        bool past = false;
+        if (a.streams) {
+            const StreamDesc& S = a.streams[a.c_stream[f]];
+            past = S.valid_total && a.c_out[f] - S.out_base >= S.total;
+        }
+        const bool ok = !past && (!a.err || a.err[f] == 0) && end >= pos + 3 && end <= a.in_size;
         if (!ok) {
             if (lane == 0) a.bad[f] = 0;
             continue;

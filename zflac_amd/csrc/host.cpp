@@ -160,6 +160,7 @@ int depth_bits_h(uint32_t dcode, int si_bps) {
 
 struct FrameHdrH {
     uint32_t bs = 0, rate = 0, chan_code = 0, dcode = 0, byte1 = 0;
+    uint32_t hdr_len = 0;  // header bytes, CRC-8 included (when err == 0 and !crc_eof)
     int err = 0;       // before the consistency checks
     bool crc_eof = false;
 };
@@ -220,6 +221,7 @@ FrameHdrH parse_frame_header_h(const uint8_t* p, uint64_t avail, uint32_t si_rat
         h.rate = T[rc];
     }
     if (avail <= idx) h.crc_eof = true;
+    h.hdr_len = (uint32_t)idx + 1;
     return h;
 }
 
@@ -276,10 +278,10 @@ struct Class {
     std::vector<ChunkDesc> chunks;
     uint64_t in_bytes = 0, out_elems = 0;
     uint32_t cap = 0;
-    // decode launches the class's data never needs, learned from its last completed run
-    // (DecodeArgs::skip_mask; 0 until a run has completed): the buckets are a function of the
-    // input bytes alone, which a batch never changes
-    uint32_t skip_mask = 0;
+    // decode launches given a full grid (DecodeArgs::full_mask): the buckets predicted from
+    // the first subframe of each member's first frame, at batch creation (plan_buckets)
+    uint32_t full_mask = 0;
+    bool redone = false;  // the last run re-ran the class (candidate table regrown)
     DevBuf<uint8_t> in;
     DevBuf<uint8_t> out;
     DevBuf<StreamDesc> d_desc;
@@ -322,13 +324,20 @@ struct zflac_batch {
     hipEvent_t front_join = nullptr;
     std::vector<zflac::StreamState> streams;
     std::vector<std::unique_ptr<zflac::Class>> classes;
-    hipEvent_t ev[8] = {};
+    hipEvent_t ev[10] = {};
     bool have_timing = false;
     bool ran = false;        // results exist only after a completed batch_run / batch_wait
     bool submitted = false;  // batch_submit enqueued a run that batch_wait has not finished
     double submit_t0 = 0;    // host clock at submit (run_wall_ms)
     zflac::DevBuf<zflac::Md5Job> md5_jobs;
     zflac::DevBuf<uint32_t> md5_dig;
+    // ZFLAC_FLAG_DEVICE_MD5: k_md5 over every certifiable stream, enqueued by submit behind
+    // the run's k_verify (pipe_who[k] = stream of job k, longest first); its digests land in
+    // pinned memory with the run's other read-backs
+    zflac::DevBuf<zflac::Md5Job> pipe_jobs;
+    zflac::DevBuf<uint32_t> pipe_dig;
+    std::vector<uint32_t> pipe_who;
+    uint32_t* pipe_pin = nullptr;
     zflac_timings timings = {};
     ~zflac_batch() {
         if (stream) (void)hipStreamSynchronize(stream);  // a submitted run may still use the buffers
@@ -337,6 +346,7 @@ struct zflac_batch {
         for (auto& s : streams) s.override_out.reset();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
+        if (pipe_pin) (void)hipHostFree(pipe_pin);
         if (stream) (void)hipStreamDestroy(stream);
         if (front) (void)hipStreamDestroy(front);
         if (front_join) (void)hipEventDestroy(front_join);
@@ -391,8 +401,13 @@ struct Uploader {
     bool used[2] = {false, false};
 };
 
-Uploader& uploader() {
-    static Uploader* u = new Uploader();  // never destroyed: outlives every batch
+// One per device: the windows' events are recorded on the streams of that device's batches.
+Uploader& uploader(int device) {
+    static std::mutex mu;
+    static std::unordered_map<int, Uploader*> per_device;  // never destroyed: outlives every batch
+    std::lock_guard<std::mutex> lock(mu);
+    Uploader*& u = per_device[device];
+    if (!u) u = new Uploader();
     return *u;
 }
 
@@ -417,9 +432,9 @@ void fill_window(uint8_t* dst, uint64_t a, uint64_t b, const std::vector<uint64_
     if (p < b) std::memset(dst + (p - a), 0, b - p);
 }
 
-void upload_streams(uint8_t* dev, uint64_t total, const std::vector<uint64_t>& in_off,
+void upload_streams(int device, uint8_t* dev, uint64_t total, const std::vector<uint64_t>& in_off,
                     const std::vector<const uint8_t*>& srcs, const std::vector<uint64_t>& lens, hipStream_t st) {
-    Uploader& U = uploader();
+    Uploader& U = uploader(device);
     std::lock_guard<std::mutex> lock(U.mu);
     for (int k = 0; k < 2; k++) {
         if (!U.pin[k]) ck(hipHostMalloc(reinterpret_cast<void**>(&U.pin[k]), Uploader::WIN, hipHostMallocDefault));
@@ -444,7 +459,26 @@ void upload_streams(uint8_t* dev, uint64_t total, const std::vector<uint64_t>& i
     ck(hipStreamSynchronize(st));
 }
 
+// The k_decode buckets (history size MB, MIX for constant / verbatim subframes) that get a
+// full grid: predicted from the first subframe of each member's first frame, whose type byte
+// follows the frame header (src/zflac.zig:426-429). k_decode classifies every frame group
+// itself; the prediction only sizes the launches (bucket_grid in decode.inc).
+uint32_t plan_buckets(const zflac_batch* b, const Class& C, const zflac_stream* src) {
+    uint32_t mask = bucket_bit(8, false);
+    for (uint32_t i : C.members) {
+        const StreamState& s = b->streams[i];
+        const uint64_t p = s.frames_begin + s.first.hdr_len;
+        if (s.first.crc_eof || p >= s.len) continue;
+        const uint32_t t = (src[i].data[p] >> 1) & 63;
+        const uint32_t ord = t >= 32 ? t - 31 : (t >= 8 && t <= 12 ? t - 8 : 0);
+        if (t <= 1) mask |= bucket_bit(8, true) | bucket_bit(32, true);  // the wave's order is unknown
+        else mask |= bucket_bit(ord <= 4 ? 4 : ord <= 8 ? 8 : ord <= 16 ? 16 : 32, false);
+    }
+    return mask;
+}
+
 void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
+    C.full_mask = plan_buckets(b, C, src);
     const int esz = esz_of_kind(C.kind);
     // input layout: each stream 16-byte aligned
     std::vector<uint64_t> in_off(C.members.size());
@@ -506,7 +540,7 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
         srcs[m] = src[C.members[m]].data;
         lens[m] = b->streams[C.members[m]].len;
     }
-    upload_streams(C.in.p, C.in.n, in_off, srcs, lens, b->stream);  // inputs resident in HBM
+    upload_streams(b->device, C.in.p, C.in.n, in_off, srcs, lens, b->stream);  // inputs resident in HBM
     C.d_desc.alloc(C.desc.size());
     ck(hipMemcpy(C.d_desc.p, C.desc.data(), C.desc.size() * sizeof(StreamDesc), hipMemcpyHostToDevice));
     const size_t nc = std::max<size_t>(C.chunks.size(), 1);
@@ -603,7 +637,7 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     if (timing_last) ck(hipEventRecord(b->ev[1], st));
     DecodeArgs da = decode_args(C);
     da.bucket_used = C.misc.p + 2;
-    da.skip_mask = C.skip_mask;
+    da.full_mask = C.full_mask;
     ck(launch_decode(C.kind, da, C.cap, b->stream, timing_last ? b->ev[4] : nullptr, b->front, b->front_join));
     st = b->stream;  // decode, verify and the read-backs
     if (timing_last) ck(hipEventRecord(b->ev[2], st));
@@ -894,7 +928,8 @@ void finish_stream_sequential(zflac_batch* b, Class& C, uint32_t slot, const std
     s.info.bits_per_sample = (uint8_t)bps0;
 }
 
-void run_md5_device(zflac_batch* b, bool timing);
+void run_md5_device(zflac_batch* b, const std::vector<uint32_t>& which, bool timing);
+void finish_md5(zflac_batch* b, bool timing);
 
 // Phase 1 of a run: every class's parallel pipeline on the batch's stream, no host wait.
 // Two batches submitted back to back overlap on the device (each has its own stream and
@@ -904,8 +939,16 @@ void submit_batch(zflac_batch* b) {
     const bool timing = (b->flags & ZFLAC_FLAG_TIMING) != 0;
     for (size_t ci = 0; ci < b->classes.size(); ci++) {
         Class& C = *b->classes[ci];
+        C.redone = false;
         alloc_candidates(C);
         enqueue_class(b, C, timing && ci == 0, timing && ci + 1 == b->classes.size());
+    }
+    if (!b->pipe_who.empty()) {  // STREAMINFO MD5 of the streams this run certifies
+        const uint32_t n = (uint32_t)b->pipe_who.size();
+        if (timing) ck(hipEventRecord(b->ev[8], b->stream));
+        ck(launch_md5(b->pipe_jobs.p, n, b->pipe_dig.p, b->stream));
+        if (timing) ck(hipEventRecord(b->ev[9], b->stream));
+        ck(hipMemcpyAsync(b->pipe_pin, b->pipe_dig.p, (size_t)n * 16, hipMemcpyDeviceToHost, b->stream));
     }
 }
 
@@ -922,11 +965,10 @@ void finish_batch(zflac_batch* b) {
             if (!C.h_misc[1] && C.h_misc[0] <= C.cap) break;
             C.cap = std::max<uint32_t>(C.h_misc[0] + 1024, C.cap * 2);  // candidate table overflow: grow, redo
             alloc_candidates(C);
-            C.skip_mask = 0;
+            C.redone = true;
             enqueue_class(b, C, false, false);
             ck(hipStreamSynchronize(b->stream));
         }
-        if (!C.h_misc[1] && C.h_misc[0] <= C.cap) C.skip_mask = 0x3Fu & ~C.h_misc[2];
     }
     const bool crc = (b->flags & ZFLAC_FLAG_CHECK_CRC16) != 0;
     b->timings.crc16_ms = 0;
@@ -942,6 +984,9 @@ void finish_batch(zflac_batch* b) {
             a.pos = C.c_pos.p;
             a.end = C.c_end.p;
             a.err = C.c_err.p;
+            a.streams = C.d_desc.p;
+            a.c_stream = C.c_stream.p;
+            a.c_out = C.c_out.p;
             a.n_frames = C.misc.p;
             a.cap = C.cap;
             a.bad = C.crc_bad.p;
@@ -993,7 +1038,8 @@ void finish_batch(zflac_batch* b) {
                 s.info.channels = (uint8_t)s.nch;
                 s.info.sample_rate = s.first.rate;
                 s.info.bits_per_sample = (uint8_t)depth_bits_h(s.first.dcode, (int)s.si.bps);
-                if (crc) {  // a certified stream's candidates are exactly its frames
+                if (crc) {  // a certified stream's candidates up to its total are exactly its frames
+                            // (k_crc16 passes the ones past the total: zflac never reads them)
                     if (h_off.empty()) {
                         h_off.resize(C.chunks.size() + 1);
                         ck(hipMemcpy(h_off.data(), C.chunk_off.p, h_off.size() * 4, hipMemcpyDeviceToHost));
@@ -1024,7 +1070,7 @@ void finish_batch(zflac_batch* b) {
         frames += std::min(C.h_misc[0], C.cap);
     }
     b->timings.md5_ms = 0;
-    if (b->flags & ZFLAC_FLAG_DEVICE_MD5) run_md5_device(b, timing && !b->classes.empty());
+    if (b->flags & ZFLAC_FLAG_DEVICE_MD5) finish_md5(b, timing && !b->classes.empty());
     else
         for (auto& s : b->streams) s.md5_dev = 0;
     b->timings.frames = frames;
@@ -1134,40 +1180,87 @@ int read_samples(zflac_batch* b, StreamState& s, void* out, bool hash) {
     return ok ? E_OK : E_INVALID_CHECKSUM;
 }
 
-// STREAMINFO MD5 of every decoded stream on the device (k_md5, one lane per stream),
-// ZFLAC_FLAG_DEVICE_MD5. A mismatch becomes the stream's error, as decode() returns
-// InvalidChecksum (src/zflac.zig:279-280).
-void run_md5_device(zflac_batch* b, bool timing) {
-    std::vector<Md5Job> jobs;
-    std::vector<uint32_t> who;
-    for (size_t i = 0; i < b->streams.size(); i++) {
-        StreamState& s = b->streams[i];
-        s.md5_dev = 0;
-        if (s.err || !s.dev_samples) continue;
-        Md5Job j{};
-        j.data = static_cast<const uint8_t*>(s.dev_samples);
-        j.n = s.info.n_samples;
-        const uint32_t js = justify_of(s.si.bps);
-        j.js = js;
-        if (s.kind == 0) {
-            j.mode = MD5_RAW, j.width = 1;
-        } else if (s.kind == 1) {
-            j.mode = js ? MD5_S16_SHIFT : MD5_RAW, j.width = 2;
-        } else if ((s.si.bps + 7) / 8 * 8 == 24) {
-            j.mode = MD5_S24, j.width = 3;
-        } else {
-            j.mode = js ? MD5_S32_SHIFT : MD5_RAW, j.width = 4;
-        }
-        jobs.push_back(j);
-        who.push_back((uint32_t)i);
+// k_md5 job of stream s over `n` samples at `data` (device), as zflac hashes them.
+Md5Job md5_job(const StreamState& s, const void* data, uint64_t n, const uint32_t* status) {
+    Md5Job j{};
+    j.data = static_cast<const uint8_t*>(data);
+    j.n = n;
+    j.status = status;
+    const uint32_t js = justify_of(s.si.bps);
+    j.js = js;
+    if (s.kind == 0) {
+        j.mode = MD5_RAW, j.width = 1;
+    } else if (s.kind == 1) {
+        j.mode = js ? MD5_S16_SHIFT : MD5_RAW, j.width = 2;
+    } else if ((s.si.bps + 7) / 8 * 8 == 24) {
+        j.mode = MD5_S24, j.width = 3;
+    } else {
+        j.mode = js ? MD5_S32_SHIFT : MD5_RAW, j.width = 4;
     }
-    if (jobs.empty()) return;
-    // longest messages first: the lanes of a wave then run chains of similar length
+    return j;
+}
+
+// Order of `jobs` longest message first: the lanes of a wave then run chains of similar length.
+std::vector<uint32_t> longest_first(const std::vector<Md5Job>& jobs) {
     std::vector<uint32_t> ord(jobs.size());
     for (uint32_t k = 0; k < ord.size(); k++) ord[k] = k;
     std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
         return jobs[x].n * jobs[x].width > jobs[y].n * jobs[y].width;
     });
+    return ord;
+}
+
+// Digest words (k_md5 layout) -> the stream's verdict; a mismatch becomes its error, as
+// decode() returns InvalidChecksum (src/zflac.zig:279-280).
+void take_digest(StreamState& s, const uint32_t* d) {
+    for (int w = 0; w < 4; w++)
+        for (int q = 0; q < 4; q++) s.md5_dig[4 * w + q] = (uint8_t)(d[w] >> (8 * q));
+    s.md5_dev = std::memcmp(s.md5_dig, s.si.md5, 16) == 0 ? 1 : 2;
+    if (s.md5_dev == 2) s.err = E_INVALID_CHECKSUM;
+}
+
+// ZFLAC_FLAG_DEVICE_MD5 at batch creation: one k_md5 job per stream the parallel pass can
+// certify (STREAMINFO total known), over its region of the class output, gated on the run's
+// k_verify status; submit enqueues them behind the run (pipelined: the hash of one batch runs
+// beside the decode of the others in flight).
+void plan_md5_pipeline(zflac_batch* b) {
+    std::vector<Md5Job> jobs;
+    std::vector<uint32_t> who;
+    for (auto& cp : b->classes) {
+        Class& C = *cp;
+        const int esz = esz_of_kind(C.kind);
+        for (size_t m = 0; m < C.members.size(); m++) {
+            const StreamDesc& D = C.desc[m];
+            if (!D.valid_total) continue;
+            jobs.push_back(md5_job(b->streams[C.members[m]], C.out.p + D.out_base * esz, D.total, C.status.p + m));
+            who.push_back(C.members[m]);
+        }
+    }
+    if (jobs.empty()) return;
+    const std::vector<uint32_t> ord = longest_first(jobs);
+    std::vector<Md5Job> sorted(jobs.size());
+    b->pipe_who.resize(jobs.size());
+    for (size_t k = 0; k < ord.size(); k++) {
+        sorted[k] = jobs[ord[k]];
+        b->pipe_who[k] = who[ord[k]];
+    }
+    b->pipe_jobs.alloc(sorted.size());
+    b->pipe_dig.alloc(sorted.size() * 4);
+    ck(hipMemcpy(b->pipe_jobs.p, sorted.data(), sorted.size() * sizeof(Md5Job), hipMemcpyHostToDevice));
+    ck(hipHostMalloc(reinterpret_cast<void**>(&b->pipe_pin), sorted.size() * 16, hipHostMallocDefault));
+}
+
+// STREAMINFO MD5 of the streams `which` on the device (k_md5, one lane per stream),
+// synchronously: the streams the pipelined hash could not cover (decoded by the sequential
+// planner, or re-run after a candidate-table regrowth).
+void run_md5_device(zflac_batch* b, const std::vector<uint32_t>& which, bool timing) {
+    std::vector<Md5Job> jobs;
+    for (uint32_t i : which) {
+        const StreamState& s = b->streams[i];
+        jobs.push_back(md5_job(s, s.dev_samples, s.info.n_samples, nullptr));
+    }
+    if (jobs.empty()) return;
+    const std::vector<uint32_t> ord = longest_first(jobs);
     std::vector<Md5Job> sorted(jobs.size());
     for (size_t k = 0; k < ord.size(); k++) sorted[k] = jobs[ord[k]];
     b->md5_jobs.alloc(sorted.size());
@@ -1183,15 +1276,36 @@ void run_md5_device(zflac_batch* b, bool timing) {
     if (timing) {
         float t = 0;
         ck(hipEventElapsedTime(&t, b->ev[5], b->ev[6]));
-        b->timings.md5_ms = t;
+        b->timings.md5_ms += t;
     }
-    for (size_t k = 0; k < ord.size(); k++) {
-        StreamState& s = b->streams[who[ord[k]]];
-        for (int w = 0; w < 4; w++)
-            for (int q = 0; q < 4; q++) s.md5_dig[4 * w + q] = (uint8_t)(dig[k * 4 + w] >> (8 * q));
-        s.md5_dev = std::memcmp(s.md5_dig, s.si.md5, 16) == 0 ? 1 : 2;
-        if (s.md5_dev == 2) s.err = E_INVALID_CHECKSUM;
+    for (size_t k = 0; k < ord.size(); k++) take_digest(b->streams[which[ord[k]]], &dig[k * 4]);
+}
+
+// After a run: the pipelined digests of the streams the run certified, then a synchronous
+// k_md5 for every other decoded stream.
+void finish_md5(zflac_batch* b, bool timing) {
+    std::vector<char> done(b->streams.size(), 0);
+    for (auto& s : b->streams) s.md5_dev = 0;
+    if (!b->pipe_who.empty()) {
+        if (timing) {
+            float t = 0;
+            ck(hipEventElapsedTime(&t, b->ev[8], b->ev[9]));
+            b->timings.md5_ms = t;
+        }
+        for (size_t k = 0; k < b->pipe_who.size(); k++) {
+            const uint32_t i = b->pipe_who[k];
+            StreamState& s = b->streams[i];
+            const Class& C = *b->classes[s.cls];
+            if (s.err || !s.dev_samples || C.redone || C.h_status[s.slot] != 0 || (b->flags & ZFLAC_FLAG_FORCE_SLOW))
+                continue;
+            take_digest(s, b->pipe_pin + k * 4);
+            done[i] = 1;
+        }
     }
+    std::vector<uint32_t> rest;
+    for (uint32_t i = 0; i < b->streams.size(); i++)
+        if (!done[i] && !b->streams[i].err && b->streams[i].dev_samples) rest.push_back(i);
+    run_md5_device(b, rest, timing);
 }
 
 int create_batch(const zflac_stream* streams, size_t n, int device, int flags, zflac_batch** out) {
@@ -1239,6 +1353,7 @@ int create_batch(const zflac_stream* streams, size_t n, int device, int flags, z
             b->classes[ci]->members.push_back((uint32_t)i);
         }
         for (auto& C : b->classes) alloc_class(b.get(), *C, streams);
+        if (flags & ZFLAC_FLAG_DEVICE_MD5) plan_md5_pipeline(b.get());
         b->timings.upload_ms = now_ms() - t1;
         // streams resolved on the host
         for (auto& s : b->streams) {
@@ -1253,6 +1368,8 @@ int create_batch(const zflac_stream* streams, size_t n, int device, int flags, z
         return E_DEVICE;
     } catch (const std::bad_alloc&) {
         return E_OUT_OF_MEMORY;
+    } catch (const std::exception&) {  // e.g. std::system_error from an upload helper thread
+        return E_DEVICE;
     }
     *out = b.release();
     return E_OK;
@@ -1297,10 +1414,19 @@ int zflac_hip_device_count(void) {
     return n;
 }
 
-const char* zflac_hip_version(void) { return "zflac_hip gfx950 r1"; }
+const char* zflac_hip_version(void) { return "zflac_hip gfx950 r3"; }
 
 int zflac_hip_batch_create(const zflac_stream* streams, size_t n, int device, int flags, zflac_batch** out) {
     return create_batch(streams, n, device, flags, out);
+}
+
+// After a failed submit: the work already enqueued (on the batch stream and, with
+// ZFLAC_FRONT_PRIORITY, the front stream) may still use the candidate buffers a retry
+// reallocates.
+static void drain_failed_submit(zflac_batch* b) {
+    (void)hipStreamSynchronize(b->stream);
+    if (b->front) (void)hipStreamSynchronize(b->front);
+    b->submitted = false;
 }
 
 int zflac_hip_batch_submit(zflac_batch* b) {
@@ -1311,13 +1437,14 @@ int zflac_hip_batch_submit(zflac_batch* b) {
         b->submitted = true;
         submit_batch(b);
     } catch (const DeviceError&) {
-        (void)hipStreamSynchronize(b->stream);
-        b->submitted = false;
+        drain_failed_submit(b);
         return E_DEVICE;
     } catch (const std::bad_alloc&) {
-        (void)hipStreamSynchronize(b->stream);
-        b->submitted = false;
+        drain_failed_submit(b);
         return E_OUT_OF_MEMORY;
+    } catch (const std::exception&) {
+        drain_failed_submit(b);
+        return E_DEVICE;
     }
     return E_OK;
 }
@@ -1333,6 +1460,8 @@ int zflac_hip_batch_wait(zflac_batch* b) {
         return E_DEVICE;
     } catch (const std::bad_alloc&) {
         return E_OUT_OF_MEMORY;
+    } catch (const std::exception&) {
+        return E_DEVICE;
     }
     return E_OK;
 }
@@ -1367,6 +1496,8 @@ int zflac_hip_batch_read(zflac_batch* b, size_t i, void* out, size_t out_bytes, 
         return read_samples(b, s, out, verify_md5 && !s.md5_dev);  // InvalidChecksum at :279-280
     } catch (const DeviceError&) {
         return E_DEVICE;
+    } catch (const std::exception&) {  // std::system_error: the hashing thread could not start
+        return E_DEVICE;
     }
 }
 
@@ -1379,10 +1510,19 @@ int zflac_hip_batch_md5(zflac_batch* b, size_t i, uint8_t* digest) {
 }
 
 int zflac_hip_batch_timings(zflac_batch* b, zflac_timings* t) {
-    if (!b || !t) return E_INVALID_ARGUMENT;
-    *t = b->timings;  // the host wall-clock fields are always filled
-    return b->have_timing ? E_OK : E_INVALID_ARGUMENT;
+    return zflac_hip_batch_timings_ex(b, t, ZFLAC_TIMINGS_V1_SIZE);
 }
+
+int zflac_hip_batch_timings_ex(zflac_batch* b, zflac_timings* t, size_t size) {
+    if (!b || !t || size == 0) return E_INVALID_ARGUMENT;
+    // the caller's struct may be older (shorter) or newer (longer) than this library's
+    std::memcpy(t, &b->timings, std::min(size, sizeof(zflac_timings)));
+    if (size > sizeof(zflac_timings)) std::memset(reinterpret_cast<uint8_t*>(t) + sizeof(zflac_timings), 0,
+                                                  size - sizeof(zflac_timings));
+    return b->have_timing ? E_OK : E_INVALID_ARGUMENT;  // the host wall-clock fields are always filled
+}
+
+int zflac_hip_abi_version(void) { return ZFLAC_HIP_ABI_VERSION; }
 
 #ifdef ZFLAC_PROBE
 // Timing-probe build only (tools/probe.sh): cycle counters the decode kernels accumulate

@@ -9,7 +9,13 @@
 // MD5 (RFC 1321) is a chain over 64-byte blocks, so one stream is one lane: a batch of
 // many streams fills waves, one long stream does not (the host keeps the CPU hash for
 // that case, see host.cpp). Per block: 16 message words from HBM (loaded one unit ahead
-// of the compression that uses them), 64 dependent rounds of ~5 VALU ops.
+// of the compression that uses them), 64 dependent rounds of ~5 VALU ops (gfx950's
+// v_bitop3_b32 makes each round function one instruction).
+//
+// A lane's time is its stream's chain (~4 cycles per VALU op for one wave alone), so a
+// batch's hash takes about as long as its longest stream, whatever the stream count; the
+// batch API enqueues it behind the decode of the same run (zflac_hip_batch_submit), so the
+// runs of other batches in flight fill the SIMDs meanwhile.
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -98,56 +104,87 @@ __device__ uint32_t message_byte(const Md5Job& j, uint64_t v) {
     }
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int UNIT_WORDS = 64;  // raw dwords per unit: 4 blocks, or 3 blocks of 24-bit samples
 
-// The full units of one stream: 256 raw bytes each, loaded one unit (3-4 blocks of
-// compression, several microseconds) ahead of their use. Returns message bytes hashed.
+// Compress one unit (UNIT_WORDS raw dwords, plus the dword after it for unaligned bases).
 template <int MODE>
+__device__ __forceinline__ void hash_unit(const uint32_t* cur, uint32_t sh, uint32_t js, uint32_t st[4]) {
+    uint32_t m[16];
+    if constexpr (MODE == MD5_S24) {
+#pragma unroll
+        for (int blk = 0; blk < 3; blk++) {
+#pragma unroll
+            for (int w = 0; w < 16; w++) {
+                // 4 samples -> 3 words: x0|x1<<24, x1>>8|x2<<16, x2>>16|x3<<8
+                const int g = blk * 16 + w, ph = g % 3, s0 = (g / 3) * 4 + ph;
+                const uint32_t x0 = (uint32_t)((int32_t)cur[s0] >> js) & 0xffffffu;
+                const uint32_t x1 = (uint32_t)((int32_t)cur[s0 + 1] >> js) & 0xffffffu;
+                m[w] = ph == 0 ? (x0 | (x1 << 24)) : ph == 1 ? ((x0 >> 8) | (x1 << 16)) : ((x0 >> 16) | (x1 << 8));
+            }
+            compress(st, m);
+        }
+    } else {
+#pragma unroll
+        for (int blk = 0; blk < 4; blk++) {
+#pragma unroll
+            for (int w = 0; w < 16; w++)
+                m[w] = unjustify_word<MODE>(sh ? __builtin_amdgcn_alignbyte(cur[blk * 16 + w + 1], cur[blk * 16 + w], sh)
+                                               : cur[blk * 16 + w],
+                                            js);
+            compress(st, m);
+        }
+    }
+}
+
+// The full units of one stream: 256 raw bytes each, loaded one unit (3-4 blocks of
+// compression, several microseconds) ahead of their use, into two register sets used in
+// turn (no copies between them). A 16-byte aligned stream (every certified stream: regions
+// start on 32-byte boundaries) loads each unit with 16 dwordx4 loads; otherwise 65 dwords.
+// Returns message bytes hashed.
+template <int MODE, bool VEC>
 __device__ __forceinline__ uint64_t hash_units(const Md5Job& j, uint32_t st[4]) {
     constexpr uint64_t MSG_PER_UNIT = MODE == MD5_S24 ? 192 : 256;
     const uint64_t L = j.n * (uint64_t)j.width;
     const uint64_t nu = L / MSG_PER_UNIT;
-    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(j.data) & 3);
+    const uint32_t sh = VEC ? 0u : (uint32_t)(reinterpret_cast<uintptr_t>(j.data) & 3);
     const uint32_t* p = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(j.data) & ~(uintptr_t)3);
-    uint32_t cur[UNIT_WORDS + 1], nxt[UNIT_WORDS + 1];
+    uint32_t ba[UNIT_WORDS + 1], bb[UNIT_WORDS + 1];
     auto load = [&](uint64_t u, uint32_t* r) {
         const uint32_t* q = p + u * UNIT_WORDS;
+        if constexpr (VEC) {
 #pragma unroll
-        for (int i = 0; i < UNIT_WORDS; i++) r[i] = __builtin_nontemporal_load(q + i);
-        // the dword after the unit carries its last bytes when the base is unaligned
-        r[UNIT_WORDS] = (MODE != MD5_S24 && sh) ? __builtin_nontemporal_load(q + UNIT_WORDS) : 0u;
-    };
-    if (nu) load(0, cur);
-    for (uint64_t u = 0; u < nu; u++) {
-        if (u + 1 < nu) load(u + 1, nxt);
-        uint32_t m[16];
-        if constexpr (MODE == MD5_S24) {
-#pragma unroll
-            for (int blk = 0; blk < 3; blk++) {
-#pragma unroll
-                for (int w = 0; w < 16; w++) {
-                    // 4 samples -> 3 words: x0|x1<<24, x1>>8|x2<<16, x2>>16|x3<<8
-                    const int g = blk * 16 + w, ph = g % 3, s0 = (g / 3) * 4 + ph;
-                    const uint32_t x0 = (uint32_t)((int32_t)cur[s0] >> j.js) & 0xffffffu;
-                    const uint32_t x1 = (uint32_t)((int32_t)cur[s0 + 1] >> j.js) & 0xffffffu;
-                    m[w] = ph == 0 ? (x0 | (x1 << 24)) : ph == 1 ? ((x0 >> 8) | (x1 << 16)) : ((x0 >> 16) | (x1 << 8));
-                }
-                compress(st, m);
+            for (int i = 0; i < UNIT_WORDS / 4; i++) {
+                const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q) + i);
+                r[4 * i] = v[0];
+                r[4 * i + 1] = v[1];
+                r[4 * i + 2] = v[2];
+                r[4 * i + 3] = v[3];
             }
+            r[UNIT_WORDS] = 0u;
         } else {
 #pragma unroll
-            for (int blk = 0; blk < 4; blk++) {
-#pragma unroll
-                for (int w = 0; w < 16; w++)
-                    m[w] = unjustify_word<MODE>(
-                        __builtin_amdgcn_alignbyte(cur[blk * 16 + w + 1], cur[blk * 16 + w], sh), j.js);
-                compress(st, m);
-            }
+            for (int i = 0; i < UNIT_WORDS; i++) r[i] = __builtin_nontemporal_load(q + i);
+            // the dword after the unit carries its last bytes when the base is unaligned
+            r[UNIT_WORDS] = (MODE != MD5_S24 && sh) ? __builtin_nontemporal_load(q + UNIT_WORDS) : 0u;
         }
-#pragma unroll
-        for (int i = 0; i <= UNIT_WORDS; i++) cur[i] = nxt[i];
+    };
+    if (nu) load(0, ba);
+    uint64_t u = 0;
+    for (; u + 2 <= nu; u += 2) {
+        load(u + 1, bb);
+        hash_unit<MODE>(ba, sh, j.js, st);
+        if (u + 2 < nu) load(u + 2, ba);
+        hash_unit<MODE>(bb, sh, j.js, st);
     }
+    if (u < nu) hash_unit<MODE>(ba, sh, j.js, st);
     return nu * MSG_PER_UNIT;
+}
+
+template <int MODE>
+__device__ __forceinline__ uint64_t hash_units_any(const Md5Job& j, uint32_t st[4]) {
+    return (reinterpret_cast<uintptr_t>(j.data) & 15) == 0 ? hash_units<MODE, true>(j, st)
+                                                          : hash_units<MODE, false>(j, st);
 }
 
 __global__ __launch_bounds__(64) void k_md5(const Md5Job* __restrict__ jobs, uint32_t n_jobs,
@@ -156,13 +193,18 @@ __global__ __launch_bounds__(64) void k_md5(const Md5Job* __restrict__ jobs, uin
     if (t >= n_jobs) return;
     const Md5Job j = jobs[t];
     uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    if (j.status && *j.status) {  // not certified by this run: the host hashes it after the planner
+#pragma unroll
+        for (int i = 0; i < 4; i++) digests[(uint64_t)t * 4 + i] = 0u;
+        return;
+    }
     const uint64_t L = j.n * (uint64_t)j.width;  // message bytes
     uint64_t done;                                // message bytes hashed by the unit loop
     switch (j.mode) {
-        case MD5_RAW: done = hash_units<MD5_RAW>(j, st); break;
-        case MD5_S16_SHIFT: done = hash_units<MD5_S16_SHIFT>(j, st); break;
-        case MD5_S32_SHIFT: done = hash_units<MD5_S32_SHIFT>(j, st); break;
-        default: done = hash_units<MD5_S24>(j, st); break;
+        case MD5_RAW: done = hash_units_any<MD5_RAW>(j, st); break;
+        case MD5_S16_SHIFT: done = hash_units_any<MD5_S16_SHIFT>(j, st); break;
+        case MD5_S32_SHIFT: done = hash_units_any<MD5_S32_SHIFT>(j, st); break;
+        default: done = hash_units_any<MD5_S24>(j, st); break;
     }
     // tail: remaining message bytes, 0x80, zero fill, 64-bit little-endian bit length
     uint32_t m[16];
