@@ -168,6 +168,11 @@ void zflac_hip_batch_destroy(zflac_batch *b);
  * (ahead of a later frame's error and of the MD5 check, which come after it in zflac's
  * read order). */
 #define ZFLAC_FLAG_CHECK_CRC16 8
+/* Subframe-start walk of 2+ channel streams: by default the library picks k_walk (a lane per
+ * frame) for launches of many frames and k_walk_wave (a wave per frame, wave-wide bit scan)
+ * otherwise. These force one (testing, timing); results are identical. */
+#define ZFLAC_FLAG_WALK_LANE 16
+#define ZFLAC_FLAG_WALK_WAVE 32
 
 const char *zflac_hip_error_name(int code);
 /* Number of HIP devices visible; 0 means every decode will fail with ZFLAC_E_DEVICE. */

@@ -290,3 +290,61 @@ def test_pipelined_device_md5_overlapped(gpu_ready):
         assert bs[0].timings().md5_ms > 0
     for b in bs:
         b.close()
+
+
+_WALK_CASES = ["c3_ms16_lpc8", "c4_24bit_lpc32_wasted", "ch3_16", "ch6_24_wasted", "ch8_16_fixed", "stereo32",
+               "longcodes24_k16", "longcodes16_k3", "ms20_lpc16_escape", "ls16_fixed_mix", "uncommon_po15",
+               "auto_stereo_lpc12", "stereo12_ms", "uncommon_block65535", "lpc32_16bit"]
+
+
+@pytest.mark.parametrize("walk", ["lane", "wave"])
+def test_both_walks_parity(gpu_ready, walk):
+    """k_walk (lane per frame) and k_walk_wave (wave per frame, wave-wide Rice scan) give the
+    same subframe starts: every parity config with 2+ channels, plus the malformed cases,
+    decoded in one batch under each walk, equal to the oracle (errors included)."""
+    names = [n for n in _WALK_CASES if n in PARITY_CONFIGS]
+    datas = [synth.generate(**dict(PARITY_CONFIGS[n], seed=4500 + i)).flac for i, n in enumerate(names)]
+    datas += [_CASES[c][0] for c in sorted(_CASES)]
+    b = zflac_amd.Batch(datas, walk=walk)
+    b.run()
+    for i, data in enumerate(datas):
+        r = oracle.decode(data)
+        try:
+            d = b.read(i)
+            err = "OK"
+        except errors.ZflacError as e:
+            err, d = type(e).__name__, None
+        assert err == r.error, (walk, i)
+        if d is not None:
+            np.testing.assert_array_equal(d.samples.values, r.samples)
+    b.close()
+
+
+@pytest.mark.parametrize("walk", ["lane", "wave"])
+def test_both_walks_mutants(gpu_ready, walk):
+    """Bit-flip mutants of the C3 / C4 fixtures under each walk: the walk must never read out
+    of bounds or hang on garbage, and the frame's error is the oracle's."""
+    import random
+
+    rng = random.Random(4600)
+    bases = [synth.generate(**dict(PARITY_CONFIGS[n], seed=4601)).flac for n in ("c3_ms16_lpc8", "c4_24bit_lpc32_wasted")]
+    datas = []
+    for k in range(60):
+        d = bytearray(bases[k % 2])
+        for _ in range(1 + k % 3):
+            p = rng.randrange(60, len(d))
+            d[p] ^= 1 << rng.randrange(8)
+        datas.append(bytes(d))
+    b = zflac_amd.Batch(datas, walk=walk)
+    b.run()
+    for i, data in enumerate(datas):
+        r = oracle.decode(data)
+        try:
+            d = b.read(i)
+            err = "OK"
+        except errors.ZflacError as e:
+            err, d = type(e).__name__, None
+        assert err == r.error, (walk, i)
+        if d is not None:
+            np.testing.assert_array_equal(d.samples.values, r.samples)
+    b.close()

@@ -49,6 +49,7 @@ ROWS = {
                                  noise_lsb=1e6), 256, 4096, False),
     "6-channel 24-bit LPC-10": (dict(channels=6, bps=24, order=10, precision=14, block_size=B, noise_lsb=64.0), 128,
                                 2048, False),
+    "C3, 2600 frames (a ~4-minute track)": (synth.config_c3(), 2600, 2600, False),
     "C3, total unknown (sequential planner)": (synth.config_c3(), 256, 4096, True),
     "C3, planted false syncs (repair path)": (dict(channels=2, bps=16, stereo_mode=1, order=8, block_size=B,
                                                    plant_sync_every=2), 256, 4096, False),
@@ -58,7 +59,7 @@ ROWS = {
 }
 
 
-def run_row(name, cfg, seg, frames, unknown, steps):
+def run_row(name, cfg, seg, frames, unknown, steps, walk=None):
     st = synth.generate(**dict(cfg, n_samples=B * seg, seed=cfg.get("seed", 7)))
     reps = max(1, frames // seg)
     if unknown == "bad_crc8":  # one generated stream, every header CRC-8 flipped
@@ -70,7 +71,7 @@ def run_row(name, cfg, seg, frames, unknown, steps):
         data = synth.tile_flac(st, reps, unknown_total=unknown)
     n = st.pcm.size * reps
     # device-resident batch runs
-    b = zflac_amd.Batch([data], timing=True)
+    b = zflac_amd.Batch([data], timing=True, walk=walk)
     for _ in range(2):
         b.run()
     walls, tms = [], []
@@ -105,7 +106,7 @@ def run_row(name, cfg, seg, frames, unknown, steps):
     wall = float(np.median(walls))
     mean = lambda f: round(float(np.mean([f(t) for t in tms])), 4)  # noqa: E731
     return {
-        "row": name, "frames": seg * reps, "channel_samples": int(n), "compressed_bytes": len(data),
+        "row": name, "walk": walk or "auto", "frames": seg * reps, "channel_samples": int(n), "compressed_bytes": len(data),
         "device_msps": round(n / wall / 1e6, 1), "device_wall_ms": round(wall * 1e3, 3),
         "scan_ms": mean(lambda t: t.scan_ms), "walk_ms": mean(lambda t: t.walk_ms),
         "decode_ms": mean(lambda t: t.decode_ms), "verify_ms": mean(lambda t: t.verify_ms),
@@ -121,14 +122,17 @@ def main():
     ap.add_argument("--rows", help="comma-separated substrings of row names (default: all)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--out")
+    ap.add_argument("--walk", default="auto", help="auto, lane, wave, or both (each row twice)")
+    ap.add_argument("--no-e2e", action="store_true")
     a = ap.parse_args()
     sel = [r for r in ROWS if not a.rows or any(x in r for x in a.rows.split(","))]
     rows = []
     for name in sel:
         cfg, seg, frames, unknown = ROWS[name]
-        r = run_row(name, cfg, seg, frames, unknown, a.steps)
-        print(json.dumps(r), flush=True)
-        rows.append(r)
+        for w in (["lane", "wave"] if a.walk == "both" else [None if a.walk == "auto" else a.walk]):
+            r = run_row(name, cfg, seg, frames, unknown, a.steps, w)
+            print(json.dumps(r), flush=True)
+            rows.append(r)
     if a.out:
         with open(a.out, "w") as f:
             json.dump({"rows": rows}, f, indent=1)

@@ -65,6 +65,8 @@ FLAG_TIMING = 1
 FLAG_FORCE_SLOW = 2
 FLAG_DEVICE_MD5 = 4
 FLAG_CHECK_CRC16 = 8  # beyond zflac (src/zflac.zig:548-551 ignores the trailer)
+FLAG_WALK_LANE = 16
+FLAG_WALK_WAVE = 32
 
 _lib = None
 

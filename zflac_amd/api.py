@@ -108,7 +108,7 @@ class Batch:
     """
 
     def __init__(self, streams, device: int = 0, timing: bool = False, force_slow: bool = False,
-                 device_md5: bool = False, check_crc16: bool = False):
+                 device_md5: bool = False, check_crc16: bool = False, walk: str | None = None):
         self._L = _lib.load()
         self._bufs = [bytes(s) for s in streams]
         arr = (_lib.zflac_stream * len(self._bufs))()
@@ -119,7 +119,8 @@ class Batch:
             arr[i].data = ctypes.cast(cb, ctypes.c_void_p)
             arr[i].len = len(b)
         flags = ((_lib.FLAG_TIMING if timing else 0) | (_lib.FLAG_FORCE_SLOW if force_slow else 0)
-                 | (_lib.FLAG_DEVICE_MD5 if device_md5 else 0) | (_lib.FLAG_CHECK_CRC16 if check_crc16 else 0))
+                 | (_lib.FLAG_DEVICE_MD5 if device_md5 else 0) | (_lib.FLAG_CHECK_CRC16 if check_crc16 else 0)
+                 | {None: 0, "lane": _lib.FLAG_WALK_LANE, "wave": _lib.FLAG_WALK_WAVE}[walk])
         self._h = ctypes.c_void_p()
         rc = self._L.zflac_hip_batch_create(arr, len(self._bufs), device, flags, ctypes.byref(self._h))
         self._keep = None  # the library copied the bytes to HBM

@@ -72,6 +72,12 @@ constexpr uint64_t CHUNK_BYTES = (uint64_t)SCAN_THREADS * SCAN_BYTES_PER_THREAD;
 constexpr int CHUNK_CAP = 64;           // candidates kept per chunk by the scan pass
 constexpr uint64_t INPUT_PAD = 4096;    // zero bytes after the last stream
 constexpr int MAX_CH = 8;               // FLAC channel limit; k_walk's per-frame record stride
+// Launches walking fewer (frames x leading subframes) than this use k_walk_wave (a wave per
+// frame) instead of k_walk (a lane per frame): below it k_walk leaves most SIMDs idle.
+#ifndef ZFLAC_WAVE_WALK_MAX_FRAMES
+#define ZFLAC_WAVE_WALK_MAX_FRAMES 16384
+#endif
+constexpr uint64_t WAVE_WALK_MAX_FRAMES = ZFLAC_WAVE_WALK_MAX_FRAMES;
 constexpr uint64_t DUMMY_BYTES = 64 * 64 * 32;  // 64 wave slots x 64 lanes x 2 quads
 constexpr uint64_t PROBE_BYTES = 256;           // after the dummy region: timing-probe builds only
 
@@ -125,13 +131,17 @@ struct DecodeArgs {
     uint32_t* group_mb;   // [frame group of a k_decode wave]: its history bucket, written by the
                           // first bucket launch so the later launches skip other groups cheaply
     uint32_t* bucket_used;  // optional: the first bucket launch ORs in bucket_bit() of every group
-    uint32_t full_mask;     // host only: bucket_bit()s launched with a grid covering every frame
-                            // group (the buckets the host predicts from the input bytes); the
-                            // others get a small grid whose waves stride over the groups, so a
-                            // bucket the data never uses costs a near-empty launch (0 = all full)
+    uint32_t full_mask;     // host only: bucket_bit()s that get their own launch, with a grid
+                            // covering every frame group (the order-8 launch, which classifies
+                            // every group, and the buckets the host predicts from the input
+                            // bytes); 0 = every bucket
+    uint32_t rest;          // set on the one extra launch (of the most general kernel, order 32
+                            // with constant / verbatim lanes) that decodes the frame groups of
+                            // every bucket outside full_mask
 };
 
-// Grid (workgroups) of a k_decode bucket launch outside DecodeArgs::full_mask.
+// Grid (workgroups) of the `rest` launch: a few waves striding over the frame groups, so
+// when the prediction holds it costs one near-empty launch.
 constexpr uint32_t SPARSE_DECODE_BLOCKS = 64;
 
 // Bit of a k_decode launch (history bucket MB, MIX kernels) in DecodeArgs::bucket_used /

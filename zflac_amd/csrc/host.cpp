@@ -37,16 +37,38 @@ ZFLAC_DECL_LAUNCH(0)
 ZFLAC_DECL_LAUNCH(1)
 ZFLAC_DECL_LAUNCH(2)
 #undef ZFLAC_DECL_LAUNCH
-// k_walk (subframe start offsets, 2+ channels) then k_decode; `mid` (optional) is recorded
-// between the two launches. With a `front` stream the walk runs there and k_decode waits for
-// it on `st` through the event `join`.
+hipError_t launch_walk_wave(int kind, const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
+
+// Which subframe-start walk a launch over `frames` frames of `nch` channels uses: k_walk
+// (lane per frame: 64 serial chains per wave) needs tens of thousands of frames to fill the
+// chip; k_walk_wave (wave per frame, wave-wide bit scan of each Rice partition) fills it with
+// a few thousand, and walks the nch - 1 leading subframes of 3..8-channel frames with a
+// short chain each. ZFLAC_WALK=lane / wave forces one (timing experiments).
+static bool use_wave_walk(uint64_t frames, int nch, int flags) {
+    static const int forced = [] {
+        const char* e = std::getenv("ZFLAC_WALK");
+        return !e ? 0 : (e[0] == 'w' ? 1 : (e[0] == 'l' ? 2 : 0));
+    }();
+    if (flags & ZFLAC_FLAG_WALK_WAVE) return true;
+    if (flags & ZFLAC_FLAG_WALK_LANE) return false;
+    if (forced) return forced == 1;
+    return nch > 2 || frames * (uint64_t)(nch - 1) < WAVE_WALK_MAX_FRAMES;
+}
+
+// k_walk or k_walk_wave (subframe start offsets, 2+ channels) then k_decode; `mid`
+// (optional) is recorded between the two launches. With a `front` stream the walk runs
+// there and k_decode waits for it on `st` through the event `join`. `est_frames`: the
+// frame count the walk choice is made for (the launch grid is sized for `max_frames`).
 static hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_frames, hipStream_t st,
-                                hipEvent_t mid = nullptr, hipStream_t front = nullptr, hipEvent_t join = nullptr) {
+                                hipEvent_t mid = nullptr, hipStream_t front = nullptr, hipEvent_t join = nullptr,
+                                uint64_t est_frames = 0, int flags = 0) {
     const int lay = a.nch == 2 ? 2 : (a.nch == 1 ? 1 : 0);
     hipStream_t ws = front ? front : st;
     if (a.nch > 1) {
-        const hipError_t e = kind == 0 ? launch_walk_k0(a, max_frames, ws)
-                                       : (kind == 1 ? launch_walk_k1(a, max_frames, ws) : launch_walk_k2(a, max_frames, ws));
+        hipError_t e;
+        if (use_wave_walk(est_frames ? est_frames : max_frames, a.nch, flags)) e = launch_walk_wave(kind, a, max_frames, ws);
+        else e = kind == 0 ? launch_walk_k0(a, max_frames, ws)
+                           : (kind == 1 ? launch_walk_k1(a, max_frames, ws) : launch_walk_k2(a, max_frames, ws));
         if (e != hipSuccess) return e;
     }
     if (mid) {
@@ -278,6 +300,7 @@ struct Class {
     std::vector<ChunkDesc> chunks;
     uint64_t in_bytes = 0, out_elems = 0;
     uint32_t cap = 0;
+    uint64_t est_frames = 0;  // frames expected from the STREAMINFO totals (walk choice)
     // decode launches given a full grid (DecodeArgs::full_mask): the buckets predicted from
     // the first subframe of each member's first frame, at batch creation (plan_buckets)
     uint32_t full_mask = 0;
@@ -562,6 +585,7 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     C.h_misc = C.pin.p;
     C.h_status = C.pin.p + 4;
     C.cap = (uint32_t)std::min<uint64_t>(est_frames + C.chunks.size() * 2 + 1024, 0x7FFFFFFFull);
+    C.est_frames = est_frames;
 }
 
 void alloc_candidates(Class& C) {
@@ -638,7 +662,8 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     DecodeArgs da = decode_args(C);
     da.bucket_used = C.misc.p + 2;
     da.full_mask = C.full_mask;
-    ck(launch_decode(C.kind, da, C.cap, b->stream, timing_last ? b->ev[4] : nullptr, b->front, b->front_join));
+    ck(launch_decode(C.kind, da, C.cap, b->stream, timing_last ? b->ev[4] : nullptr, b->front, b->front_join,
+                     C.est_frames, b->flags));
     st = b->stream;  // decode, verify and the read-backs
     if (timing_last) ck(hipEventRecord(b->ev[2], st));
     VerifyArgs va;
@@ -728,7 +753,7 @@ struct SeqRunner {
         a.sub_start = p_sub.p;
         p_mb.alloc(n / 4 + 2);
         a.group_mb = p_mb.p;
-        ck(launch_decode(C.kind, a, (uint32_t)n, st));
+        ck(launch_decode(C.kind, a, (uint32_t)n, st, nullptr, nullptr, nullptr, 0, b->flags));
         std::vector<uint64_t> e(n);
         std::vector<int32_t> er(n);
         std::vector<uint32_t> in(n), ra(n);
