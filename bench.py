@@ -87,7 +87,10 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-md5", action="store_true", help="skip the device-MD5 leg")
-    ap.add_argument("--md5-inflight", type=int, default=4, help="batches in flight in the decode+MD5 leg")
+    ap.add_argument("--md5-inflight", type=int, default=8, help="batches in flight in the decode+MD5 leg")
+    ap.add_argument("--md5-hw-queues", type=int, default=16,
+                    help="GPU_MAX_HW_QUEUES of the decode+MD5 leg's process (one HIP stream per batch in flight)")
+    ap.add_argument("--md5-leg-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-e2e", action="store_true", help="skip the single-stream decode() legs")
     ap.add_argument("--e2e-frames", type=int, default=65536, help="frames of the long single stream")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default=None)
@@ -274,6 +277,72 @@ def e2e_leg(name: str, cfg: dict, seg_frames: int, frames: int, oracle_full: boo
             "md5_bound_msps": round(n / (tm["host_md5_ms"] * 1e-3) / 1e6, 1) if tm["host_md5_ms"] else None}
 
 
+def md5_leg(args, streams, device: int, barrier=lambda: None):
+    """decode + STREAMINFO MD5 of every stream of the shard: batches created with
+    ZFLAC_FLAG_DEVICE_MD5, whose k_md5 zflac_hip_batch_submit enqueues right behind each
+    run's kernels; `md5_inflight` batches round robin, so one batch's hash (a serial chain
+    per stream, ~7 ms for this shard) runs beside the other batches' runs."""
+    import zflac_amd
+
+    k_md5 = max(1, min(args.md5_inflight, args.steps))
+    mbs = [zflac_amd.Batch(streams, device=device, timing=True, device_md5=True) for _ in range(k_md5)]
+    rec = []
+
+    def done(j):
+        mbs[j].wait()
+        rec.append(mbs[j].timings().md5_ms)
+
+    def steps(k):
+        pending = [False] * len(mbs)
+        for i in range(k):
+            j = i % len(mbs)
+            if pending[j]:
+                done(j)
+            mbs[j].submit()
+            pending[j] = True
+        for t in range(len(mbs)):
+            j = (k + t) % len(mbs)
+            if pending[j]:
+                done(j)
+
+    steps(max(args.warmup, k_md5))
+    rec.clear()
+    barrier()
+    t1 = time.perf_counter()
+    steps(args.steps)
+    barrier()
+    el = time.perf_counter() - t1
+    samples = mbs[0].timings().samples
+    out_bytes = mbs[0].timings().output_bytes
+    ok = all(mb.info(i)[0] == 0 and mb.md5(i) == s[26:42] for mb in mbs for i, s in enumerate(streams))
+    for mb in mbs:
+        mb.close()
+    return {"kernel": "k_md5", "md5_ms": round(float(np.mean(rec)), 4), "all_match": ok, "inflight": k_md5,
+            "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+            "decode_plus_md5_msps_rank0": round(samples * args.steps / el / 1e6, 1),
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "md5_waves_per_simd": round(k_md5 * -(-len(streams) // 64) / 1024, 3),
+            "hashed_bytes_rank0": int(out_bytes),
+            "note": "decode + STREAMINFO MD5 of every stream, k_md5 (one lane per stream) enqueued behind each "
+                    "run; md5_ms = k_md5 launch time while overlapped; not in `value`"}
+
+
+def md5_leg_in_child(args):
+    """Run md5_leg in a child process (same rank, same shard) with GPU_MAX_HW_QUEUES set, so
+    the headline's process keeps the runtime's defaults. Returns its dict (None on failure)."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--md5-leg-child", "--steps", str(args.steps), "--warmup",
+           str(args.warmup), "--streams-per-gpu", str(args.streams_per_gpu), "--md5-inflight", str(args.md5_inflight)]
+    if args.same_device:
+        cmd.append("--same-device")
+    env = dict(os.environ)
+    env.setdefault("GPU_MAX_HW_QUEUES", str(args.md5_hw_queues))
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True)
+    if r.returncode != 0:
+        print(r.stderr[-2000:], file=sys.stderr)
+        return None
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 # ------------------------------------------------------------------------ main
 def main():
     args = parse_args()
@@ -281,6 +350,11 @@ def main():
     if env_world is None and args.gpus and args.gpus > 1:
         sys.exit(launch(args.gpus))
     world = int(env_world or 1)
+    if args.md5_leg_child:  # the decode+MD5 leg of this rank, in its own process (md5_leg_in_child)
+        rank = int(os.environ.get("RANK", "0"))
+        device = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
+        print(json.dumps(md5_leg(args, make_shard(rank, world, args.streams_per_gpu), device)), flush=True)
+        return
     if args.gpus is not None and args.gpus != world:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
@@ -404,52 +478,14 @@ def main():
     ok = tot.errors == 0
 
     # decode() also checks the STREAMINFO MD5 (src/zflac.zig:267-280): the same shard with
-    # ZFLAC_FLAG_DEVICE_MD5, whose k_md5 submit enqueues right behind each run's kernels;
-    # `md5_inflight` batches round robin, so one batch's hash runs beside the others' decode
+    # ZFLAC_FLAG_DEVICE_MD5, in a child process of its own whose GPU_MAX_HW_QUEUES covers
+    # one hardware queue per batch in flight (md5_leg)
     md5 = None
     if not args.no_md5:
         batch.close()
         batch = None
-        k_md5 = max(1, min(args.md5_inflight, args.steps))
-        mbs = [zflac_amd.Batch(streams, device=device, timing=True, device_md5=True) for _ in range(k_md5)]
-        md5_rec = []
-
-        def md5_done(j):
-            mbs[j].wait()
-            md5_rec.append(mbs[j].timings().md5_ms)
-
-        def md5_steps(k):
-            pending = [False] * len(mbs)
-            for i in range(k):
-                j = i % len(mbs)
-                if pending[j]:
-                    md5_done(j)
-                mbs[j].submit()
-                pending[j] = True
-            for t in range(len(mbs)):
-                j = (k + t) % len(mbs)
-                if pending[j]:
-                    md5_done(j)
-
-        md5_steps(max(args.warmup, k_md5))
-        md5_rec.clear()
-        barrier_sync()
-        t1 = time.perf_counter()
-        md5_steps(args.steps)
-        barrier_sync()
-        el_md5 = time.perf_counter() - t1
-        md5_ok = all(mb.info(i)[0] == 0 and mb.md5(i) == s[26:42] for mb in mbs for i, s in enumerate(streams))
-        for mb in mbs:
-            mb.close()
-        m_avg = float(np.mean(md5_rec))
-        md5 = {"kernel": "k_md5", "md5_ms": round(m_avg, 4), "all_match": md5_ok, "inflight": k_md5,
-               "decode_plus_md5_msps_rank0": round(samples_rank * args.steps / el_md5 / 1e6, 1),
-               "ms_per_step": round(el_md5 / args.steps * 1e3, 4),
-               "md5_waves_per_simd": round(k_md5 * -(-len(streams) // 64) / 1024, 3),
-               "hashed_bytes_rank0": int(out_bytes),
-               "note": "decode + STREAMINFO MD5 of every stream, k_md5 (one lane per stream) enqueued "
-                       "behind each run; md5_ms = k_md5 launch time while overlapped; not in `value`"}
-        ok = ok and md5_ok
+        md5 = md5_leg_in_child(args)
+        ok = ok and bool(md5 and md5.get("all_match"))
 
     cpu = None
     e2e = None

@@ -42,6 +42,18 @@ __device__ inline void scan_window(const uint8_t* in, uint64_t ws, uint64_t lo, 
     scan_window_v(*reinterpret_cast<const uint4*>(in + ws), in, ws, lo, hi, fn);
 }
 
+// A wave's 16-byte windows are consecutive per lane, so the 16 bytes after a lane's window
+// are the next lane's window (DPP wave_shl:1); lane 63, and a lane whose next window lies
+// past the chunk (zeroed), read them from memory.
+// (Call at wave-uniform points: DPP reads the neighbour lane's registers.)
+__device__ __forceinline__ uint32_t lane_above(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, true);  // wave_shl:1
+}
+
+// k_scan: one workgroup per 32 KiB chunk. Every lane's 8 windows are loaded at once; a
+// candidate's header (at most 16 bytes from its sync code) is parsed from the lane's
+// window and the next one, staged in the lane's own 32-byte LDS slot: no dependent global
+// reads, which previously kept each workgroup alive for several memory round trips.
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     const uint32_t chunk = blockIdx.x;
     if (chunk >= a.n_chunks) return;
@@ -49,13 +61,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     __shared__ unsigned long long s_units;
     __shared__ uint64_t s_pos[CHUNK_CAP];
     __shared__ uint32_t s_u[CHUNK_CAP];
+    __shared__ uint8_t s_crc[256];
+    __shared__ uint4 s_hdr[SCAN_THREADS][2];  // a lane's window and the next one (candidates only)
     const ChunkDesc ch = a.chunks[chunk];
-    const StreamDesc S = a.streams[ch.stream];
-    if (threadIdx.x == 0) {
-        s_cnt = 0;
-        s_units = 0;
-    }
-    __syncthreads();
     const uint64_t abase = ch.begin & ~(uint64_t)15;
     // all of the thread's windows in flight at once (coalesced 4 KiB rows per round)
     constexpr int R = SCAN_BYTES_PER_THREAD / 16;
@@ -65,13 +73,47 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
         const uint64_t ws = abase + ((uint64_t)r * SCAN_THREADS + threadIdx.x) * 16;
         v[r] = ws < ch.end ? *reinterpret_cast<const uint4*>(a.in + ws) : make_uint4(0, 0, 0, 0);
     }
+    const StreamDesc S = a.streams[ch.stream];
+    if (threadIdx.x == 0) {
+        s_cnt = 0;
+        s_units = 0;
+    }
+    s_crc[threadIdx.x & 255u] = CRC8.t[threadIdx.x & 255u];
+    __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; r++) {
         const uint64_t ws = abase + ((uint64_t)r * SCAN_THREADS + threadIdx.x) * 16;
-        if (ws >= ch.end) break;
-        scan_window_v(v[r], a.in, ws, ch.begin, ch.end, [&](uint64_t p) {
-            const FrameHdr h = parse_frame_header(a.in + p, S.in_end - p, S.si_rate);
-            if (!candidate_ok(h, S)) return;
+        uint32_t ff = 0;  // bit b: byte b is 0xFF
+        ff |= (ff_mask(v[r].x) * 0x00204081u) >> 28 & 15u;
+        ff |= ((ff_mask(v[r].y) * 0x00204081u) >> 28 & 15u) << 4;
+        ff |= ((ff_mask(v[r].z) * 0x00204081u) >> 28 & 15u) << 8;
+        ff |= ((ff_mask(v[r].w) * 0x00204081u) >> 28 & 15u) << 12;
+        // the wave's windows are contiguous: a sync code in byte 15 needs the next window
+        const bool live = ws < ch.end;
+        const bool need_next = live && ff != 0;
+        const uint32_t n0 = lane_above(v[r].x), n1 = lane_above(v[r].y), n2 = lane_above(v[r].z),
+                       n3 = lane_above(v[r].w);
+        const bool nx_mem = (threadIdx.x & 63u) == 63u || ws + 16 >= ch.end;  // DPP value is not the next window
+        if (!need_next) continue;
+        const uint32_t nfirst = ((ff >> 15) && nx_mem) ? a.in[ws + 16] : n0;
+        bool staged = false;
+        while (ff) {
+            const uint32_t b = (uint32_t)__ffs(ff) - 1u;
+            ff &= ff - 1u;
+            const uint32_t q = (b + 1) >> 2;  // dword of byte b + 1 (4 = the next window's first)
+            const uint32_t dw = q == 0 ? v[r].x : q == 1 ? v[r].y : q == 2 ? v[r].z : q == 3 ? v[r].w : nfirst;
+            const uint32_t nb = (dw >> (8 * ((b + 1) & 3))) & 0xFFu;
+            const uint64_t p = ws + b;
+            if ((nb & 0xFE) != 0xF8 || p < ch.begin || p >= ch.end) continue;
+            if (!staged) {
+                s_hdr[threadIdx.x][0] = v[r];
+                s_hdr[threadIdx.x][1] = nx_mem ? *reinterpret_cast<const uint4*>(a.in + ws + 16) : make_uint4(n0, n1, n2, n3);
+                staged = true;
+            }
+            const uint8_t* hb = reinterpret_cast<const uint8_t*>(&s_hdr[threadIdx.x][0]) + b;
+            const FrameHdr h = parse_frame_header_t<true>([hb](uint32_t i) -> uint32_t { return hb[i]; },
+                                                          S.in_end - p, S.si_rate, s_crc);
+            if (!candidate_ok(h, S)) continue;
             const uint32_t slot = atomicAdd(&s_cnt, 1u);
             const uint32_t units = h.bs * S.nch;
             atomicAdd(&s_units, (unsigned long long)units);
@@ -79,7 +121,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
                 s_pos[slot] = p;
                 s_u[slot] = units;
             }
-        });
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -10,14 +10,17 @@
 //
 // Subframe headers, warm-up / coefficient skips and partition headers are read
 // wave-uniformly. The Rice codes of a partition (src/zflac.zig:655-664: unary q, a 1, k
-// bits) are found by a wave-wide scan of the next 2048 bits: lane i takes word i and, for
-// an entry offset e, follows the codes through its word (clz per code: ffs over the word)
-// to the offset x where the next code starts in word i+1, recording the set V of code
-// starts it visited. Entries are guessed and corrected (Jacobi rounds with a ballot for
+// bits) are found by a wave-wide scan of the next 4096 bits: lane i takes words 2i, 2i+1 and, for
+// an entry offset e, follows the codes through its two words (clz per code: ffs over the
+// segment) to the offset x where the next code starts in lane i+1's segment, recording the
+// set V of code starts it visited. Entries are guessed and corrected (Jacobi rounds with a ballot for
 // convergence): lane i's entry is lane i-1's exit; if it is in V the lane's chain has
 // already merged with the true one, otherwise the lane re-runs from it. Rice codes
 // resynchronise within a few codes, so a few rounds settle all 64 lanes. The codes each lane
 // completes are then summed by a wave prefix scan, which locates the partition's last code.
+// Lane i scans two words (64 bits, ~7 codes at C3's k): a chain from a wrong entry merges
+// with the true one within the segment ~70 % of the time, so ~4 rounds settle the wave, and
+// one pass covers 4096 bits, a whole partition of C3.
 #include "device_common.h"
 
 namespace zflac {
@@ -44,14 +47,16 @@ struct WKind<2> {
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// The frame's bytes as big-endian words, a 128-word window: lane i holds words wb + i (cur)
-// and wb + 64 + i (nxt). Word indices count from the frame's 16-byte aligned base; loads
-// past the input buffer read zeros (buffer range check).
+// The frame's bytes as big-endian words, a 320-word window: lane i holds words wb + 64 m + i
+// in r_m. Words wb .. wb + 191 are read (r0..r2); r3, r4 are in flight for the next 128
+// words, so a pass that moves on by a whole 4096-bit scan finds them resident. Word indices
+// count from the frame's 16-byte aligned base; loads past the input buffer read zeros
+// (buffer range check).
 struct WaveWin {
     __amdgpu_buffer_rsrc_t rs;
     uint32_t nwords;  // words inside the buffer resource
     uint32_t wb;      // wave-uniform
-    uint32_t cur, nxt;
+    uint32_t r0, r1, r2, r3, r4;
 
     __device__ __forceinline__ uint32_t load(uint32_t w) const {
         const uint32_t off = w < nwords ? w * 4u : 0x80000000u;
@@ -59,28 +64,32 @@ struct WaveWin {
     }
     __device__ __forceinline__ void init(uint32_t w0) {
         wb = uni(w0);
-        cur = load(wb + lane_id());
-        nxt = load(wb + 64u + lane_id());
+        r0 = load(wb + lane_id());
+        r1 = load(wb + 64u + lane_id());
+        r2 = load(wb + 128u + lane_id());
+        r3 = load(wb + 192u + lane_id());
+        r4 = load(wb + 256u + lane_id());
     }
     __device__ __forceinline__ void slide() {
-        cur = nxt;
+        r0 = r1;
+        r1 = r2;
+        r2 = r3;
+        r3 = r4;
         wb = uni(wb + 64u);
-        nxt = load(wb + 64u + lane_id());
+        r4 = load(wb + 256u + lane_id());
     }
-    // make words w and w+1 resident (w only grows)
+    // make words w .. w + 127 readable: w - wb < 64 (w only grows)
     __device__ __forceinline__ void reach(uint32_t w) {
-        if (w + 1u >= wb + 128u) {
-            if (w >= wb + 64u && w < wb + 128u) {
-                slide();
-            } else {
-                init(w);
-            }
-        }
+        for (int i = 0; i < 4 && w >= wb + 64u; i++) slide();
+        if (w >= wb + 64u) init(w);
     }
-    __device__ __forceinline__ uint32_t word(uint32_t w) const {  // wb <= w < wb + 128, uniform
+    __device__ __forceinline__ uint32_t word(uint32_t w) const {  // wb <= w < wb + 192, uniform
         const uint32_t j = uni(w - wb);
-        return j < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)j)
-                       : (uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)(j - 64u));
+        const uint32_t v = j < 64u ? r0 : (j < 128u ? r1 : r2);
+        return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(j & 63u));
+    }
+    __device__ __forceinline__ uint32_t byte(uint32_t b) const {  // byte b from the base, uniform
+        return (word(wb + (b >> 2)) >> (24u - 8u * (b & 3u))) & 0xFFu;
     }
     // the 32 bits at bit position P (MSB first)
     __device__ __forceinline__ uint32_t peek(uint32_t P) {
@@ -94,38 +103,40 @@ struct WaveWin {
         P += n;
         return v;
     }
-    // lane i gets word (P >> 5) + i (the 64 words from P's word on)
-    __device__ __forceinline__ uint32_t from(uint32_t P) {
-        const uint32_t w = P >> 5;
-        if (w >= wb + 64u) {
-            if (w < wb + 128u) slide();
-            else init(w);
-        }
-        const uint32_t j0 = uni(w - wb);
-        const int src = (int)((lane_id() + j0) & 63u);
-        const uint32_t a = (uint32_t)__shfl((int)cur, src), b = (uint32_t)__shfl((int)nxt, src);
-        return lane_id() + j0 < 64u ? a : b;
+    __device__ __forceinline__ uint32_t at(uint32_t j) const {  // window word j (< 192) to this lane
+        const int src = (int)(j & 63u);
+        const uint32_t a = (uint32_t)__shfl((int)r0, src), b = (uint32_t)__shfl((int)r1, src),
+                       c = (uint32_t)__shfl((int)r2, src);
+        return j < 64u ? a : (j < 128u ? b : c);
+    }
+    // lane i gets words (P >> 5) + 2i and + 2i + 1: the 4096 bits from P's word on
+    __device__ __forceinline__ void from(uint32_t P, uint32_t& hi, uint32_t& lo) {
+        reach(P >> 5);
+        const uint32_t j0 = uni((P >> 5) - wb);
+        hi = at(j0 + 2u * lane_id());
+        lo = at(j0 + 2u * lane_id() + 1u);
     }
 };
 
-// Codes through one word from entry offset e (0..31): V = code starts visited (bit 31 - s
-// for start s), x = start of the next code in the following word (0..31), un = the last
-// start's unary run continues past the word (its code is not counted in this word).
-__device__ __forceinline__ void chain(uint32_t w, uint32_t e, uint32_t kp1, uint32_t& V, uint32_t& x, uint32_t& un) {
+// Codes through one 64-bit segment (hi, lo) from entry offset e (0..63): V = code starts
+// visited (bit 63 - s for start s), x = start of the next code in the following segment
+// (0..31: a code's k <= 30 remainder bits end at most 31 bits past the segment), un = the
+// last start's unary run continues past the segment (its code is not counted here).
+__device__ __forceinline__ void chain(uint64_t w, uint32_t e, uint32_t kp1, uint64_t& V, uint32_t& x, uint32_t& un) {
     V = 0;
     un = 0;
     x = 0;
-    for (int it = 0; it < 33; it++) {
-        V |= 0x80000000u >> e;
-        const uint32_t m = w << e;
+    for (int it = 0; it < 65; it++) {
+        V |= 0x8000000000000000ull >> e;
+        const uint64_t m = w << e;
         if (m == 0) {
             un = 1;
             x = 0;
             break;
         }
-        const uint32_t e2 = e + (uint32_t)__builtin_clz(m) + kp1;  // terminator + 1 + k
-        if (e2 >= 32u) {
-            x = e2 - 32u;
+        const uint32_t e2 = e + (uint32_t)__builtin_clzll(m) + kp1;  // terminator + 1 + k
+        if (e2 >= 64u) {
+            x = e2 - 64u;
             break;
         }
         e = e2;
@@ -145,6 +156,11 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
     return v + (l >= 16u ? t0 : 0u) + (l >= 32u ? t1 : 0u) + (l >= 48u ? t2 : 0u);
 }
 
+// x of the lane below (DPP wave_shr:1; lane 0 gets 0)
+__device__ __forceinline__ uint32_t from_below(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, true);
+}
+
 // Skip n Rice codes of parameter k starting at bit P (src/zflac.zig:655-664). False when the
 // scan runs past `end` (the frame's decode then fails at EndOfStream anyway).
 __device__ bool skip_rice(WaveWin& W, uint32_t& P, uint32_t n, uint32_t k, uint32_t end) {
@@ -152,38 +168,43 @@ __device__ bool skip_rice(WaveWin& W, uint32_t& P, uint32_t n, uint32_t k, uint3
     const uint32_t kp1 = k + 1u;
     while (n) {
         if (P > end) return false;
-        const uint32_t w = W.from(P);
+        uint32_t hi, lo;
+        W.from(P, hi, lo);
+        const uint64_t w = ((uint64_t)hi << 32) | lo;
         const uint32_t e0 = P & 31u;
-        const uint32_t wbase = P & ~31u;  // bit position of lane 0's word
-        uint32_t V, x, un;
+        const uint32_t wbase = P & ~31u;  // bit position of lane 0's segment
+        uint64_t V;
+        uint32_t x, un;
         chain(w, lane == 0 ? e0 : 0u, kp1, V, x, un);
         uint32_t want = e0;
         for (int round = 0; round < 64; round++) {
-            const uint32_t px = (uint32_t)__shfl_up((int)x, 1);
+            const uint32_t px = from_below(x);
             want = lane == 0 ? e0 : px;
-            const bool need = lane != 0 && ((V << want) >> 31) == 0;  // want not among the visited starts
+            const bool need = lane != 0 && ((V << want) >> 63) == 0;  // want not among the visited starts
             if (__builtin_amdgcn_ballot_w64(need) == 0) break;
             if (need) chain(w, want, kp1, V, x, un);
         }
-        const uint32_t Vw = V & (0xFFFFFFFFu >> want);  // starts on the true chain
-        const uint32_t cnt = (uint32_t)__builtin_popcount(Vw) - un;
+        const uint64_t Vw = V & (~0ull >> want);  // starts on the true chain
+        const uint32_t cnt = (uint32_t)__builtin_popcountll(Vw) - un;
         const uint32_t cum = wave_scan(cnt);
         const uint32_t total = uni((uint32_t)__builtin_amdgcn_readlane((int)cum, 63));
         if (total < n) {
             n -= total;
-            P = wbase + 2048u + uni((uint32_t)__builtin_amdgcn_readlane((int)x, 63));
+            P = wbase + 4096u + uni((uint32_t)__builtin_amdgcn_readlane((int)x, 63));
             continue;
         }
         const uint64_t hit = __builtin_amdgcn_ballot_w64(cum >= n);
         const uint32_t L = uni((uint32_t)__builtin_ctzll(hit));
         const uint32_t cumL = uni((uint32_t)__builtin_amdgcn_readlane((int)cum, (int)L));
         const uint32_t cntL = uni((uint32_t)__builtin_amdgcn_readlane((int)cnt, (int)L));
-        uint32_t VL = uni((uint32_t)__builtin_amdgcn_readlane((int)Vw, (int)L));
+        const uint32_t vh = uni((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(Vw >> 32), (int)L));
+        const uint32_t vl = uni((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)Vw, (int)L));
+        uint64_t VL = ((uint64_t)vh << 32) | vl;
         const uint32_t xL = uni((uint32_t)__builtin_amdgcn_readlane((int)x, (int)L));
         // the last code is lane L's r-th counted one; it ends where the next start is
         const uint32_t r = n - (cumL - cntL);
-        for (uint32_t i = 0; i < r; i++) VL &= ~(0x80000000u >> __builtin_clz(VL));
-        P = VL ? wbase + 32u * L + (uint32_t)__builtin_clz(VL) : wbase + 32u * (L + 1u) + xL;
+        for (uint32_t i = 0; i < r; i++) VL &= ~(0x8000000000000000ull >> __builtin_clzll(VL));
+        P = VL ? wbase + 64u * L + (uint32_t)__builtin_clzll(VL) : wbase + 64u * (L + 1u) + xL;
         n = 0;
     }
     return true;
@@ -285,21 +306,24 @@ __global__ __launch_bounds__(WW_THREADS) void k_walk_wave(DecodeArgs a) {
     for (uint32_t f = uni(wave); f < nframes; f += nwaves) {
         const uint64_t pos = a.c_pos[f];
         const StreamDesc S = a.streams[a.c_stream[f]];
-        const FrameHdr h = parse_frame_fields(a.in + pos, S.in_end > pos ? S.in_end - pos : 0, S.si_rate);
-        const int bps = depth_bits(h.dcode, S.si_bps);
-        // the frame decodes only with these (setup_frame in decode.inc)
-        bool ok = !h.err && !h.crc_eof && channels_count(h.chan_code) == nch && bps >= 0;
         const uint64_t abase = pos & ~(uint64_t)15;
-        const uint64_t end_bytes = S.in_end > abase ? S.in_end - abase : 0;
-        const uint32_t end = end_bytes * 8 > 0xFFFF0000ull ? 0xFFFF0000u : (uint32_t)(end_bytes * 8);
-        uint32_t P = ((uint32_t)(pos & 15) + h.hdr_len) * 8u;
         WaveWin W;
         const uint64_t wlen = a.in_size > abase ? a.in_size - abase : 0;
         const uint32_t rbytes = (uint32_t)(wlen > 0x7FFFFFF0ull ? 0x7FFFFFF0ull : wlen);
         W.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.in) + abase, (short)0, (int)rbytes,
                                                  WBUFFER_RSRC_WORD3);
         W.nwords = rbytes / 4u;
-        W.init(P >> 5);
+        W.init(0);
+        // the frame header from the window (its at most 16 + 16 bytes are words 0..7)
+        const uint32_t hb = (uint32_t)(pos & 15);
+        const FrameHdr h = parse_frame_header_t<false>([&](uint32_t i) -> uint32_t { return W.byte(hb + i); },
+                                                       S.in_end > pos ? S.in_end - pos : 0, S.si_rate, nullptr);
+        const int bps = depth_bits(h.dcode, S.si_bps);
+        // the frame decodes only with these (setup_frame in decode.inc)
+        bool ok = !h.err && !h.crc_eof && channels_count(h.chan_code) == nch && bps >= 0;
+        const uint64_t end_bytes = S.in_end > abase ? S.in_end - abase : 0;
+        const uint32_t end = end_bytes * 8 > 0xFFFF0000ull ? 0xFFFF0000u : (uint32_t)(end_bytes * 8);
+        uint32_t P = (hb + h.hdr_len) * 8u;
         for (int c = 0; c + 1 < nch; c++) {
             if (ok) {
                 const bool side = (h.chan_code == 8 && c == 1) || (h.chan_code == 9 && c == 0) ||
