@@ -327,20 +327,26 @@ def md5_leg(args, streams, device: int, barrier=lambda: None):
                     "run; md5_ms = k_md5 launch time while overlapped; not in `value`"}
 
 
-def md5_leg_in_child(args):
-    """Run md5_leg in a child process (same rank, same shard) with GPU_MAX_HW_QUEUES set, so
-    the headline's process keeps the runtime's defaults. Returns its dict (None on failure)."""
+def start_md5_child(args):
+    """Start the process that will run md5_leg (same rank, same shard) with GPU_MAX_HW_QUEUES
+    set, so the headline's process keeps the runtime's defaults. Started before this process
+    touches the GPU (no fork / exec from a process with a GPU context); it generates its
+    shard, then waits on stdin until md5_leg_in_child tells it to start."""
     cmd = [sys.executable, os.path.abspath(__file__), "--md5-leg-child", "--steps", str(args.steps), "--warmup",
            str(args.warmup), "--streams-per-gpu", str(args.streams_per_gpu), "--md5-inflight", str(args.md5_inflight)]
     if args.same_device:
         cmd.append("--same-device")
-    env = dict(os.environ)
-    env.setdefault("GPU_MAX_HW_QUEUES", str(args.md5_hw_queues))
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True)
-    if r.returncode != 0:
-        print(r.stderr[-2000:], file=sys.stderr)
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(args.md5_hw_queues))
+    return subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+
+
+def md5_leg_in_child(proc):
+    """Let the child started by start_md5_child run its leg now; returns its dict (None on
+    failure)."""
+    out, _ = proc.communicate("go\n")
+    if proc.returncode != 0 or not out.strip():
         return None
-    return json.loads(r.stdout.strip().splitlines()[-1])
+    return json.loads(out.strip().splitlines()[-1])
 
 
 # ------------------------------------------------------------------------ main
@@ -350,10 +356,13 @@ def main():
     if env_world is None and args.gpus and args.gpus > 1:
         sys.exit(launch(args.gpus))
     world = int(env_world or 1)
-    if args.md5_leg_child:  # the decode+MD5 leg of this rank, in its own process (md5_leg_in_child)
+    if args.md5_leg_child:  # the decode+MD5 leg of this rank, in its own process (start_md5_child)
         rank = int(os.environ.get("RANK", "0"))
         device = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
-        print(json.dumps(md5_leg(args, make_shard(rank, world, args.streams_per_gpu), device)), flush=True)
+        streams = make_shard(rank, world, args.streams_per_gpu)
+        if sys.stdin.readline().strip() != "go":
+            return
+        print(json.dumps(md5_leg(args, streams, device)), flush=True)
         return
     if args.gpus is not None and args.gpus != world:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
@@ -361,6 +370,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     device = 0 if args.same_device else local_rank
     backend = args.backend or ("gloo" if (args.dry_run or args.same_device) else "nccl")
+    md5_proc = None if (args.no_md5 or args.dry_run) else start_md5_child(args)
     dist = None
     if world > 1:
         import torch
@@ -484,7 +494,7 @@ def main():
     if not args.no_md5:
         batch.close()
         batch = None
-        md5 = md5_leg_in_child(args)
+        md5 = md5_leg_in_child(md5_proc)
         ok = ok and bool(md5 and md5.get("all_match"))
 
     cpu = None

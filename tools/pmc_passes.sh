@@ -10,6 +10,6 @@ i=0
 for P in "$@"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o run -- \
-      python3 $R/bench.py --streams-per-gpu $N --steps 3 --warmup 1 --no-cpu-baseline --no-verify > $OUT/p$i.log 2>&1 || exit 1
+      python3 $R/bench.py --streams-per-gpu $N --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-md5 --no-e2e > $OUT/p$i.log 2>&1 || exit 1
 done
 echo done > $OUT/status.txt

@@ -13,4 +13,4 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- \
-    python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-e2e $EXTRA > $OUT/stats.log 2>&1
+    python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-e2e --no-md5 $EXTRA > $OUT/stats.log 2>&1

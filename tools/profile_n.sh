@@ -6,4 +6,4 @@ OUT=$R/gpurun_out/$1
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- \
-    python3 $R/bench.py --streams-per-gpu $2 --steps 10 --warmup 2 --no-cpu-baseline --no-verify > $OUT/stats.log 2>&1
+    python3 $R/bench.py --streams-per-gpu $2 --steps 10 --warmup 2 --no-cpu-baseline --no-verify --no-md5 --no-e2e > $OUT/stats.log 2>&1
