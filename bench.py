@@ -76,6 +76,11 @@ def pmc_traffic(prefix: str, lib_sha: str | None):
             "source": os.path.relpath(d.get("_source", PMC_SUMMARY), ROOT)}
 
 
+def progress(msg: str) -> None:
+    """One line per phase on stderr (long runs keep writing, so a watchdog sees progress)."""
+    print(f"bench [{time.strftime('%H:%M:%S')}] rank {os.environ.get('RANK', '0')}: {msg}", file=sys.stderr, flush=True)
+
+
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None, help="ranks (one per GPU); default WORLD_SIZE or 1")
@@ -395,6 +400,7 @@ def main():
     t_gen = time.perf_counter()
     streams = make_shard(rank, world, args.streams_per_gpu)
     t_gen = time.perf_counter() - t_gen
+    progress(f"shard of {len(streams)} streams generated in {t_gen:.1f} s")
 
     if args.dry_run:  # no GPU: the launch / shard / aggregation path only
         barrier_sync()
@@ -454,6 +460,7 @@ def main():
                 done(j)
 
     run_steps(args.warmup, batches)
+    progress("warm-up done")
     barrier_sync()
     t0 = time.perf_counter()
     rec_ov = {n: [] for n in STAGES}
@@ -475,6 +482,7 @@ def main():
         serial = (time.perf_counter() - t1) / args.steps
     scan_ms, walk_ms, dec_ms, ver_ms = (rec[n] for n in STAGES)
 
+    progress(f"timed steps done ({elapsed / args.steps * 1e3:.3f} ms/step)")
     errs = []
     n_compared = 0
     if not args.no_verify:
@@ -494,6 +502,7 @@ def main():
     if not args.no_md5:
         batch.close()
         batch = None
+        progress("verification done; decode+MD5 leg")
         md5 = md5_leg_in_child(md5_proc)
         ok = ok and bool(md5 and md5.get("all_match"))
 
@@ -501,10 +510,12 @@ def main():
     e2e = None
     if rank == 0 and world == 1:
         if not args.no_cpu_baseline:
+            progress("CPU baseline")
             cpu = cpu_baseline(streams, args.cpu_seconds)
         if not args.no_e2e:
             import synth
 
+            progress("end-to-end decode() legs")
             e2e = [e2e_leg("C3 stereo M/S 16-bit LPC-8, 65536 frames (SURVEY 8d size)", synth.config_c3(),
                            1024, args.e2e_frames, oracle_full=False),
                    e2e_leg("C3, 2600 frames (a ~4-minute track)", synth.config_c3(), 2600, 2600, oracle_full=True)]
