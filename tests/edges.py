@@ -15,6 +15,8 @@ import synth
 from .util import GOLDEN
 
 STEREO16 = dict(channels=2, bps=16, block_size=4096, order=8, n_samples=4096 * 6, seed=91)
+STEREO32 = dict(channels=2, bps=32, order=8, precision=15, block_size=4096, n_samples=4096 * 3, tone_amp=0.2,
+                noise_lsb=1e6)
 
 
 def const_side_cases():
@@ -77,6 +79,11 @@ def out_of_domain_cases():
         "decor_overflow_rs": mk(**dict(STEREO16, stereo_mode=9, fault_frame=2, fault_kind=6)),
         "decor_overflow_ms8": mk(channels=2, bps=8, stereo_mode=10, order=4, precision=7, fault_frame=1,
                                  fault_kind=6, noise_lsb=1.0, tone_amp=0.2, n_samples=4096 * 3),
+        # 32-bit containers with 32-bit samples: the fast path's wrapping i32 decorrelation
+        # must still see the overflow (src/zflac.zig:558,564,573-574)
+        "decor_overflow_ls32": mk(**dict(STEREO32, stereo_mode=8, fault_frame=1, fault_kind=6)),
+        "decor_overflow_rs32": mk(**dict(STEREO32, stereo_mode=9, fault_frame=1, fault_kind=6)),
+        "decor_overflow_ms32": mk(**dict(STEREO32, stereo_mode=10, fault_frame=1, fault_kind=6)),
         # large coefficients: LPC sums overflow the InterType (:527-532)
         "lpc_sum_overflow16": mk(channels=2, bps=16, stereo_mode=1, fault_frame=1, fault_kind=8, order=32,
                                  precision=15, tone_amp=0.9, noise_lsb=2000.0, n_samples=4096 * 3),

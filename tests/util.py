@@ -77,6 +77,13 @@ PARITY_CONFIGS = {
     "ch8_16_fixed": dict(channels=8, bps=16, predictor=2, order=2, block_size=512, n_samples=512 * 5),
     "stereo32": dict(channels=2, bps=32, stereo_mode=1, order=8, precision=15, block_size=4096,
                      n_samples=4096 * 2, tone_amp=0.2, noise_lsb=1e6),
+    # 31/32-bit stereo on the fast path (wrapping i32 decorrelation, per-sample overflow checks)
+    "stereo32_ms": dict(channels=2, bps=32, stereo_mode=10, order=8, precision=15, block_size=4096,
+                        n_samples=4096 * 2, tone_amp=0.2, noise_lsb=1e6),
+    "stereo31_ls_loud": dict(channels=2, bps=31, stereo_mode=8, order=8, precision=15, block_size=4096,
+                             n_samples=4096 * 2, tone_amp=0.45, noise_lsb=1e6),
+    "stereo32_rs": dict(channels=2, bps=32, stereo_mode=9, order=12, precision=15, block_size=2048,
+                        n_samples=2048 * 3, tone_amp=0.3, noise_lsb=1e5),
     # long Rice codes: forced k with residuals ~2^k+4, so q + 1 + k crosses 32 bits often
     "longcodes24_k16": dict(channels=2, bps=24, stereo_mode=8, order=4, precision=14, block_size=4096,
                             n_samples=4096 * 2, rice_k=16, rice2=1, noise_lsb=float(2 ** 19)),
