@@ -92,7 +92,7 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-md5", action="store_true", help="skip the device-MD5 leg")
-    ap.add_argument("--md5-inflight", type=int, default=8, help="batches in flight in the decode+MD5 leg")
+    ap.add_argument("--md5-inflight", type=int, default=12, help="batches in flight in the decode+MD5 leg")
     ap.add_argument("--md5-hw-queues", type=int, default=16,
                     help="GPU_MAX_HW_QUEUES of the decode+MD5 leg's process (one HIP stream per batch in flight)")
     ap.add_argument("--md5-leg-child", action="store_true", help=argparse.SUPPRESS)

@@ -348,3 +348,15 @@ def test_both_walks_mutants(gpu_ready, walk):
         if d is not None:
             np.testing.assert_array_equal(d.samples.values, r.samples)
     b.close()
+
+
+def test_huge_stream_multi_pass_chunk_scan(gpu_ready):
+    """One 590 MB stream (C3, 65,536 frames, the SURVEY 8(d) size): 18 Ki scan chunks, more
+    than k_scan_chunks keeps in registers per thread (16 Ki), so its grouped second pass runs;
+    decode() verifies the STREAMINFO MD5 of the whole 1 GiB output."""
+    st = synth.generate(**synth.config_c3(n_frames=1024))
+    data = synth.tile_flac(st, 64)
+    assert len(data) > 16384 * 32768
+    d = zflac_amd.decode(data)
+    assert d.samples.values.size == st.pcm.size * 64
+    np.testing.assert_array_equal(d.samples.values[: st.pcm.size], expected_samples(st))

@@ -135,14 +135,18 @@ struct DecodeArgs {
                             // covering every frame group (the order-8 launch, which classifies
                             // every group, and the buckets the host predicts from the input
                             // bytes); 0 = every bucket
-    uint32_t rest;          // set on the one extra launch (of the most general kernel, order 32
-                            // with constant / verbatim lanes) that decodes the frame groups of
-                            // every bucket outside full_mask
+    uint32_t rest;          // set on the `rest` launch (of the most general kernel, order 32 with
+                            // constant / verbatim lanes) that decodes the frame groups of every
+                            // bucket outside full_mask
+    uint32_t rest_only;     // host only: launch nothing but the rest kernel (no walk, no bucket
+                            // kernels). The normal launch never includes it: the host issues it
+                            // after a run whose order-8 launch reported a bucket outside
+                            // full_mask (bucket_used), so a correct prediction costs no launch
 };
 
-// Grid (workgroups) of the `rest` launch: a few waves striding over the frame groups, so
-// when the prediction holds it costs one near-empty launch.
-constexpr uint32_t SPARSE_DECODE_BLOCKS = 64;
+// Grid (workgroups) of the `rest` launch: a few waves striding over the frame groups (the
+// groups of unpredicted buckets; a misprediction costs time, never correctness).
+constexpr uint32_t SPARSE_DECODE_BLOCKS = 256;
 
 // Bit of a k_decode launch (history bucket MB, MIX kernels) in DecodeArgs::bucket_used /
 // full_mask: 8 -> 1, 4 -> 2, 16 -> 4, 32 -> 8, MIX 8 -> 16, MIX 32 -> 32. The order-8 launch

@@ -64,7 +64,7 @@ static hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_fram
                                 uint64_t est_frames = 0, int flags = 0) {
     const int lay = a.nch == 2 ? 2 : (a.nch == 1 ? 1 : 0);
     hipStream_t ws = front ? front : st;
-    if (a.nch > 1) {
+    if (a.nch > 1 && !a.rest_only) {
         hipError_t e;
         if (use_wave_walk(est_frames ? est_frames : max_frames, a.nch, flags)) e = launch_walk_wave(kind, a, max_frames, ws);
         else e = kind == 0 ? launch_walk_k0(a, max_frames, ws)
@@ -686,6 +686,35 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     ck(hipMemcpyAsync(C.h_misc, C.misc.p, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
 }
 
+// After a run whose order-8 launch found frame groups of a bucket the host did not
+// predict (bucket_used outside full_mask): the rest launch decodes them, then the chain
+// check and the read-backs run again (synchronous; a correct prediction never gets here).
+void enqueue_rest(zflac_batch* b, Class& C) {
+    hipStream_t st = b->stream;
+    DecodeArgs da = decode_args(C);
+    da.full_mask = C.full_mask;
+    da.rest_only = 1;
+    ck(launch_decode(C.kind, da, C.cap, st));
+    ck(hipMemsetAsync(C.status.p, 0, C.members.size() * sizeof(uint32_t), st));
+    VerifyArgs va;
+    va.streams = C.d_desc.p;
+    va.n_streams = (uint32_t)C.members.size();
+    va.chunk_off = C.chunk_off.p;
+    va.c_pos = C.c_pos.p;
+    va.c_stream = C.c_stream.p;
+    va.c_out = C.c_out.p;
+    va.n_frames = C.misc.p;
+    va.cap = C.cap;
+    va.c_end = C.c_end.p;
+    va.c_err = C.c_err.p;
+    va.c_info = C.c_info.p;
+    va.c_rate = C.c_rate.p;
+    va.status = C.status.p;
+    ck(launch_verify(va, C.cap, st));
+    ck(hipMemcpyAsync(C.h_status, C.status.p, C.members.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    ck(hipStreamSynchronize(st));
+}
+
 // ---------------------------------------------------------------------------------
 // Sequential chain planner (src/zflac.zig:340-581 state machine) for streams the
 // fast path could not certify. Frame records come from the fast pass when the chain
@@ -993,6 +1022,10 @@ void finish_batch(zflac_batch* b) {
             C.redone = true;
             enqueue_class(b, C, false, false);
             ck(hipStreamSynchronize(b->stream));
+        }
+        if (C.full_mask && (C.h_misc[2] & ~C.full_mask)) {  // a bucket without a launch was used
+            enqueue_rest(b, C);
+            C.redone = true;
         }
     }
     const bool crc = (b->flags & ZFLAC_FLAG_CHECK_CRC16) != 0;
