@@ -45,15 +45,26 @@ __device__ inline void scan_window(const uint8_t* in, uint64_t ws, uint64_t lo, 
 // A wave's 16-byte windows are consecutive per lane, so the 16 bytes after a lane's window
 // are the next lane's window (DPP wave_shl:1); lane 63, and a lane whose next window lies
 // past the chunk (zeroed), read them from memory.
+// Bit 7 of byte i set where byte i of d is 0xFF and the byte after it (byte i + 1, or the
+// first byte of dn for i = 3) is 0xF8 or 0xF9: a frame sync code (src/zflac.zig:351-352).
+// Exact per byte (no borrow between bytes).
+__device__ __forceinline__ uint32_t sync_mask(uint32_t d, uint32_t dn) {
+    const uint32_t nxt = __builtin_amdgcn_alignbyte(dn, d, 1);  // byte i = the byte after byte i of d
+    const uint32_t y = (nxt & 0xFEFEFEFEu) ^ 0xF8F8F8F8u;        // zero bytes: next is 0xF8 / 0xF9
+    const uint32_t zero = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
+    return ff_mask(d) & zero;
+}
+
 // (Call at wave-uniform points: DPP reads the neighbour lane's registers.)
 __device__ __forceinline__ uint32_t lane_above(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, true);  // wave_shl:1
 }
 
-// k_scan: one workgroup per 32 KiB chunk. Every lane's 8 windows are loaded at once. A
-// window without a 0xFF byte (~94 % of compressed data) costs four mask tests and one DPP
-// move; a sync code's next byte comes from the registers (the next window's first dword is
-// the next lane's, DPP wave_shl:1). A real candidate's header (at most 16 bytes) is parsed
+// k_scan: one workgroup per 32 KiB chunk. Every lane's 8 windows are loaded at once. Sync
+// codes (0xFF then 0xF8 / 0xF9) are found with exact per-byte SWAR masks over the window's
+// four dwords and the next window's first one (the next lane's, DPP wave_shl:1): ~40 VALU
+// per 16 bytes, and the per-candidate loop only runs at real sync codes (~1 in 64 KiB of
+// compressed data). A real candidate's header (at most 16 bytes) is parsed
 // from its window and the next one staged in the lane's own 32-byte LDS slot: no chain of
 // dependent global byte reads, which kept each workgroup alive for several memory round
 // trips.
@@ -68,14 +79,16 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     __shared__ uint4 s_hdr[SCAN_THREADS][2];  // a lane's window and the next one (candidates only)
     const ChunkDesc ch = a.chunks[chunk];
     const uint64_t abase = ch.begin & ~(uint64_t)15;
-    // all of the thread's windows in flight at once (coalesced 4 KiB rows per round)
+    // all of the thread's windows in flight at once (coalesced 4 KiB rows per round); the
+    // buffer unit answers reads past the chunk end with zeros (no per-load branch)
     constexpr int R = SCAN_BYTES_PER_THREAD / 16;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(a.in) + abase, (short)0, (int)(ch.end - abase), 0x00020000);
     uint4 v[R];
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-        const uint64_t ws = abase + ((uint64_t)r * SCAN_THREADS + threadIdx.x) * 16;
-        v[r] = ws < ch.end ? *reinterpret_cast<const uint4*>(a.in + ws) : make_uint4(0, 0, 0, 0);
-    }
+    for (int r = 0; r < R; r++)
+        v[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, threadIdx.x * 16u,
+                                                                                 r * SCAN_THREADS * 16, 0));
     const StreamDesc S = a.streams[ch.stream];
     if (threadIdx.x == 0) {
         s_cnt = 0;
@@ -87,26 +100,27 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
 #pragma unroll
     for (int r = 0; r < R; r++) {
         const uint64_t ws = lane_ws + (uint64_t)r * SCAN_THREADS * 16;
-        const uint32_t m0 = ff_mask(v[r].x), m1 = ff_mask(v[r].y), m2 = ff_mask(v[r].z), m3 = ff_mask(v[r].w);
-        const uint32_t n0 = lane_above(v[r].x);  // the next window's first dword (wave-uniform point)
-        if ((m0 | m1 | m2 | m3) == 0 || ws >= ch.end) continue;  // no 0xFF byte: the common case
-        // a wave's windows are contiguous: the next window is the next lane's, except for lane
-        // 63 and past the chunk end (zeroed there), where it is read from memory
+        // a wave's windows are contiguous: the next window's first dword is the next lane's
+        // (DPP), except for lane 63 and past the chunk end (zeroed), where a sync code in
+        // byte 15 reads its next byte from memory (rare)
+        const uint32_t n0 = lane_above(v[r].x);
+        const uint32_t c0 = sync_mask(v[r].x, v[r].y), c1 = sync_mask(v[r].y, v[r].z),
+                       c2 = sync_mask(v[r].z, v[r].w);
+        uint32_t c3 = sync_mask(v[r].w, n0);
         const bool nx_mem = (threadIdx.x & 63u) == 63u || ws + 16 >= ch.end;
-        uint32_t ff = (m0 * 0x00204081u) >> 28 & 15u;  // bit b: byte b is 0xFF
-        ff |= ((m1 * 0x00204081u) >> 28 & 15u) << 4;
-        ff |= ((m2 * 0x00204081u) >> 28 & 15u) << 8;
-        ff |= ((m3 * 0x00204081u) >> 28 & 15u) << 12;
-        const uint32_t nfirst = ((ff >> 15) && nx_mem) ? a.in[ws + 16] : n0;
+        if (nx_mem && (v[r].w >> 24) == 0xFFu && ws < ch.end)
+            c3 = (c3 & 0x00808080u) | ((a.in[ws + 16] & 0xFEu) == 0xF8u ? 0x80000000u : 0u);
+        if ((c0 | c1 | c2 | c3) == 0 || ws >= ch.end) continue;  // no sync code: the common case
+        uint32_t cand = (c0 * 0x00204081u) >> 28 & 15u;  // bit b: a sync code at byte b
+        cand |= ((c1 * 0x00204081u) >> 28 & 15u) << 4;
+        cand |= ((c2 * 0x00204081u) >> 28 & 15u) << 8;
+        cand |= ((c3 * 0x00204081u) >> 28 & 15u) << 12;
         bool staged = false;
-        while (ff) {
-            const uint32_t b = (uint32_t)__ffs(ff) - 1u;
-            ff &= ff - 1u;
-            const uint32_t q = (b + 1) >> 2;  // dword of byte b + 1 (4 = the next window's first)
-            const uint32_t dw = q == 0 ? v[r].x : q == 1 ? v[r].y : q == 2 ? v[r].z : q == 3 ? v[r].w : nfirst;
-            const uint32_t nb = (dw >> (8 * ((b + 1) & 3))) & 0xFFu;
+        while (cand) {
+            const uint32_t b = (uint32_t)__ffs(cand) - 1u;
+            cand &= cand - 1u;
             const uint64_t p = ws + b;
-            if ((nb & 0xFE) != 0xF8 || p < ch.begin || p >= ch.end) continue;
+            if (p < ch.begin || p >= ch.end) continue;
             if (!staged) {  // the header (at most 16 bytes from p) from this window and the next
                 s_hdr[threadIdx.x][0] = v[r];
                 s_hdr[threadIdx.x][1] = *reinterpret_cast<const uint4*>(a.in + ws + 16);
