@@ -130,7 +130,7 @@ def make_shard(rank: int, world: int, n_streams: int):
 
     cfgs = [synth.config_c5(g, n_frames=FRAMES_PER_STREAM) for g in shard_range(rank, world, n_streams)]
     out = [None] * n_streams
-    workers = min(16, os.cpu_count() or 1)
+    workers = host_threads(world)
 
     def work(k):
         for i in range(k, n_streams, workers):
@@ -156,6 +156,12 @@ def host_cores() -> tuple[int, str]:
     except (OSError, ValueError):
         pass
     return n, note
+
+
+def host_threads(world: int) -> int:
+    """Host threads per rank for generation and verification: the job's cores split over the
+    ranks of this node (8 ranks on a 16-core allowance would otherwise run 128 threads)."""
+    return max(1, min(16, host_cores()[0] // max(1, world)))
 
 
 def _oracle_rate(streams, seconds: float, threads: int, md5: bool):
@@ -211,7 +217,7 @@ def verify(batches, streams):
 
     errs = []
     lock = threading.Lock()
-    workers = min(16, os.cpu_count() or 1)
+    workers = host_threads(int(os.environ.get("WORLD_SIZE", "1")))
     compared = [0] * workers
 
     def work(k):

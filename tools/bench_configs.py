@@ -105,6 +105,10 @@ def run_row(name, cfg, seg, frames, unknown, steps, walk=None):
     cpu_msps = st.pcm.size * reps_cpu / t_cpu / 1e6
     wall = float(np.median(walls))
     mean = lambda f: round(float(np.mean([f(t) for t in tms])), 4)  # noqa: E731
+    # algorithmic bytes: compressed frame bytes read + PCM bytes written
+    out_bytes = n * (1 if cfg["bps"] <= 8 else 2 if cfg["bps"] <= 16 else 4)
+    alg = (len(data) - int(st.frame_offsets[0])) + out_bytes
+    dec_ms = mean(lambda t: t.decode_ms)
     return {
         "row": name, "walk": walk or "auto", "frames": seg * reps, "channel_samples": int(n), "compressed_bytes": len(data),
         "device_msps": round(n / wall / 1e6, 1), "device_wall_ms": round(wall * 1e3, 3),
@@ -114,6 +118,8 @@ def run_row(name, cfg, seg, frames, unknown, steps, walk=None):
         "e2e_breakdown_ms": {k: round(tm[k], 2) for k in ("upload_ms", "run_wall_ms", "read_ms", "host_md5_ms")},
         "oracle_1t_msps": round(cpu_msps, 1), "device_over_oracle_1t": round(n / wall / 1e6 / cpu_msps, 1),
         "e2e_over_oracle_1t": round(n / best / 1e6 / cpu_msps, 2), "bit_exact": bool(exact),
+        "alg_bytes": int(alg), "decode_kernel_frac_of_8TBs": round(alg / (dec_ms * 1e-3) / 8e12, 4) if dec_ms else None,
+        "device_run_frac_of_8TBs": round(alg / wall / 8e12, 4),
     }
 
 
@@ -123,7 +129,6 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--out")
     ap.add_argument("--walk", default="auto", help="auto, lane, wave, or both (each row twice)")
-    ap.add_argument("--no-e2e", action="store_true")
     a = ap.parse_args()
     sel = [r for r in ROWS if not a.rows or any(x in r for x in a.rows.split(","))]
     rows = []
