@@ -167,22 +167,38 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
 }
 
 // ----------------------------------------------------------------------------------
+// wave-level scans (64 lanes, __shfl_up: no workgroup barrier)
+// ----------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T wave_incl_sum(T v) {
+    const uint32_t ln = threadIdx.x & 63u;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const T y = __shfl_up(v, d, 64);
+        if (ln >= (uint32_t)d) v += y;
+    }
+    return v;
+}
+
+// ----------------------------------------------------------------------------------
 // k_scan_chunks: single-workgroup exclusive scans (n_chunks is ~input/32KiB)
 // ----------------------------------------------------------------------------------
 constexpr int SCANK_THREADS = 1024;
+constexpr int SCANK_WAVES = SCANK_THREADS / 64;
 constexpr int SCANK_PER = 16;  // chunks a thread loads at once
 
 // Thread t owns chunks [t * per, (t + 1) * per). Its counts are loaded SCANK_PER at a time
 // (independent loads: one memory latency per group, where a per-element load loop costs
-// one latency per chunk), summed, the per-thread sums scanned across the block, and the
-// offsets written on a second pass over the range (one group for batches up to 16 Ki
-// chunks = 512 MiB of input: kept in registers between the passes).
+// one latency per chunk), summed, the per-thread sums scanned in each wave (shuffles) and
+// across the 16 wave totals (one barrier), and the offsets written on a second pass over the
+// range (one group for batches up to 16 Ki chunks = 512 MiB of input: kept in registers
+// between the passes).
 __global__ __launch_bounds__(SCANK_THREADS) void k_scan_chunks(const uint32_t* cnt, const unsigned long long* units,
                                                                uint32_t n, uint32_t* off,
                                                                unsigned long long* uoff, uint32_t* n_frames) {
-    __shared__ uint32_t s_c[SCANK_THREADS];
-    __shared__ unsigned long long s_u[SCANK_THREADS];
-    const uint32_t t = threadIdx.x;
+    __shared__ uint32_t s_c[SCANK_WAVES];
+    __shared__ unsigned long long s_u[SCANK_WAVES];
+    const uint32_t t = threadIdx.x, wv = t >> 6;
     const uint32_t per = (n + SCANK_THREADS - 1) / SCANK_THREADS;
     const uint32_t lo = min(t * per, n), hi = min(lo + per, n);
     uint32_t c[SCANK_PER];
@@ -205,23 +221,24 @@ __global__ __launch_bounds__(SCANK_THREADS) void k_scan_chunks(const uint32_t* c
             su += u[i];
         }
     }
-    s_c[t] = sc;
-    s_u[t] = su;
-    __syncthreads();
-    for (uint32_t d = 1; d < SCANK_THREADS; d <<= 1) {  // Hillis-Steele inclusive
-        uint32_t vc = 0;
-        unsigned long long vu = 0;
-        if (t >= d) {
-            vc = s_c[t - d];
-            vu = s_u[t - d];
-        }
-        __syncthreads();
-        s_c[t] += vc;
-        s_u[t] += vu;
-        __syncthreads();
+    const uint32_t ic = wave_incl_sum(sc);
+    const unsigned long long iu = wave_incl_sum(su);
+    if ((t & 63u) == 63u) {
+        s_c[wv] = ic;
+        s_u[wv] = iu;
     }
-    uint32_t rc = t ? s_c[t - 1] : 0u;
-    unsigned long long ru = t ? s_u[t - 1] : 0ull;
+    __syncthreads();
+    uint32_t rc = ic - sc;
+    unsigned long long ru = iu - su;
+    for (uint32_t w = 0; w < wv; w++) {  // the waves before this one (LDS broadcasts)
+        rc += s_c[w];
+        ru += s_u[w];
+    }
+    if (t == SCANK_THREADS - 1) {
+        off[n] = rc + sc;
+        uoff[n] = ru + su;
+        *n_frames = rc + sc;
+    }
     for (uint32_t g = lo; g < hi; g += SCANK_PER) {
         if (hi - lo > (uint32_t)SCANK_PER) load(g);  // one group: still in registers
 #pragma unroll
@@ -234,47 +251,26 @@ __global__ __launch_bounds__(SCANK_THREADS) void k_scan_chunks(const uint32_t* c
             ru += u[i];
         }
     }
-    if (t == SCANK_THREADS - 1) {
-        off[n] = s_c[t];
-        uoff[n] = s_u[t];
-        *n_frames = s_c[t];
-    }
 }
 
 // ----------------------------------------------------------------------------------
 // k_compact: ordered candidate table
 // ----------------------------------------------------------------------------------
-__global__ __launch_bounds__(SCAN_THREADS) void k_compact(CompactArgs a) {
-    const uint32_t chunk = blockIdx.x;
-    if (chunk >= a.n_chunks) return;
+constexpr int COMPACT_CHUNKS = SCAN_THREADS / 64;  // chunks per workgroup: one wave each
+
+// Overflowed chunk (more than CHUNK_CAP candidates): ordered two-pass rescan of each 4 KiB
+// sub-range with a workgroup-wide exclusive scan. Called at workgroup-uniform points.
+__device__ void compact_rescan(const CompactArgs& a, uint32_t chunk) {
     const ChunkDesc ch = a.chunks[chunk];
     const StreamDesc S = a.streams[ch.stream];
-    const uint32_t n = a.chunk_cnt[chunk];
     const uint32_t off = a.chunk_off[chunk];
     const unsigned long long ubase = a.chunk_uoff[S.first_chunk];
     const unsigned long long u0 = a.chunk_uoff[chunk];
-    if (n <= CHUNK_CAP) {
-        const uint32_t t = threadIdx.x;
-        if (t < n) {
-            unsigned long long pre = 0;
-            for (uint32_t i = 0; i < t; i++) pre += a.chunk_slot_units[(uint64_t)chunk * CHUNK_CAP + i];
-            const uint32_t idx = off + t;
-            if (idx < a.cap) {
-                a.c_pos[idx] = a.chunk_slots[(uint64_t)chunk * CHUNK_CAP + t];
-                a.c_stream[idx] = ch.stream;
-                a.c_out[idx] = S.out_base + (u0 - ubase + pre);
-            } else {
-                atomicOr(a.overflow, 1u);
-            }
-        }
-        return;
-    }
-    // Overflowed chunk (more than CHUNK_CAP candidates): ordered two-pass rescan of each
-    // 4 KiB sub-range with a block-wide exclusive scan.
     __shared__ uint32_t s_c[SCAN_THREADS];
     __shared__ unsigned long long s_u[SCAN_THREADS];
     __shared__ uint32_t s_base_c;
     __shared__ unsigned long long s_base_u;
+    __syncthreads();
     if (threadIdx.x == 0) {
         s_base_c = 0;
         s_base_u = 0;
@@ -332,6 +328,41 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_compact(CompactArgs a) {
             s_base_u += s_u[threadIdx.x];
         }
         __syncthreads();
+    }
+}
+
+// One wave per chunk: lane i < n writes the chunk's i-th candidate (in position order, as
+// k_scan sorted them), its output offset = the stream's units before the chunk + the units
+// of candidates 0..i-1 (a wave prefix sum). Four chunks per workgroup: a workgroup per chunk
+// was ~40k mostly idle waves for the C5 shard's ~11k chunks. Overflowed chunks of the
+// workgroup are then rescanned by the whole workgroup, in order.
+__global__ __launch_bounds__(SCAN_THREADS) void k_compact(CompactArgs a) {
+    const uint32_t c0 = blockIdx.x * COMPACT_CHUNKS;
+    const uint32_t chunk = c0 + (threadIdx.x >> 6), ln = threadIdx.x & 63u;
+    if (chunk < a.n_chunks) {
+        const uint32_t n = a.chunk_cnt[chunk];
+        if (n <= CHUNK_CAP) {  // wave-uniform
+            const uint32_t stream = a.chunks[chunk].stream;
+            const StreamDesc& S = a.streams[stream];
+            const unsigned long long base = S.out_base + (a.chunk_uoff[chunk] - a.chunk_uoff[S.first_chunk]);
+            const uint32_t u = ln < n ? a.chunk_slot_units[(uint64_t)chunk * CHUNK_CAP + ln] : 0u;
+            const uint32_t pre = wave_incl_sum(u) - u;  // <= 64 frames x 65535 x 8 channels < 2^32
+            if (ln < n) {
+                const uint32_t idx = a.chunk_off[chunk] + ln;
+                if (idx < a.cap) {
+                    a.c_pos[idx] = a.chunk_slots[(uint64_t)chunk * CHUNK_CAP + ln];
+                    a.c_stream[idx] = stream;
+                    a.c_out[idx] = base + pre;
+                } else {
+                    atomicOr(a.overflow, 1u);
+                }
+            }
+        }
+    }
+#pragma unroll 1
+    for (uint32_t j = 0; j < (uint32_t)COMPACT_CHUNKS; j++) {  // workgroup-uniform
+        const uint32_t cj = c0 + j;
+        if (cj < a.n_chunks && a.chunk_cnt[cj] > CHUNK_CAP) compact_rescan(a, cj);
     }
 }
 
@@ -403,7 +434,8 @@ hipError_t launch_scan_chunks(const uint32_t* cnt, const unsigned long long* uni
 }
 hipError_t launch_compact(const CompactArgs& a, hipStream_t st) {
     if (a.n_chunks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_compact, dim3(a.n_chunks), dim3(SCAN_THREADS), 0, st, a);
+    hipLaunchKernelGGL(k_compact, dim3((a.n_chunks + COMPACT_CHUNKS - 1) / COMPACT_CHUNKS), dim3(SCAN_THREADS), 0, st,
+                       a);
     return hipGetLastError();
 }
 hipError_t launch_sync_list(const SyncListArgs& a, hipStream_t st) {
