@@ -10,6 +10,8 @@ note = sys.argv[3] if len(sys.argv) > 3 else ""
 rows = {}
 for f in sorted(glob.glob(os.path.join(d, "*.json"))):
     lib, run = os.path.basename(f)[:-5].rsplit("_", 1)
+    if not run.isdigit():  # not a bench line (config rows of the same call)
+        continue
     j = json.load(open(f))
     rows.setdefault(lib, []).append({"run": int(run), "value": j["value"], "ms_per_step": j["ms_per_step"],
                                      "ms_per_step_serial": j.get("ms_per_step_serial"), "stages_ms": j["stages_ms"],
