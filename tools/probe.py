@@ -1,6 +1,7 @@
 """Timing-probe run (experimental build with -DZFLAC_PROBE, tools/_build/lib_probe.so):
-cycles per chunk phase of k_walk and k_decode, summed over waves, for the C5 shard.
-Usage: ZFLAC_HIP_LIB=tools/_build/lib_probe.so python tools/probe.py [streams]"""
+cycles per chunk phase of k_walk and k_decode, summed over waves, for the C5 shard or one
+tiled stream of a BASELINE config (c2 / c3 / c4, 65,536 frames).
+Usage: ZFLAC_HIP_LIB=tools/_build/lib_probe.so python tools/probe.py [streams | c2 | c3 | c4]"""
 import ctypes
 import json
 import os
@@ -12,8 +13,16 @@ import synth  # noqa: E402
 import zflac_amd  # noqa: E402
 from zflac_amd import _lib  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 1250
-streams = [s.flac for s in synth.generate_many([synth.config_c5(i) for i in range(n)])]
+arg = sys.argv[1] if len(sys.argv) > 1 else "1250"
+if arg.isdigit():
+    n = int(arg)
+    streams = [s.flac for s in synth.generate_many([synth.config_c5(i) for i in range(n)])]
+else:
+    cfg = {"c2": synth.config_c2, "c3": synth.config_c3, "c4": synth.config_c4}[arg]()
+    seg = 512
+    st = synth.generate(**dict(cfg, n_samples=4096 * seg, seed=cfg.get("seed", 7)))
+    streams = [synth.tile_flac(st, 65536 // seg)]
+    n = arg
 b = zflac_amd.Batch(streams, timing=True)
 L = _lib.load()
 fn = L.zflac_hip_probe
