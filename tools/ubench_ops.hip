@@ -51,6 +51,32 @@ OP_KERNEL(k_mul_lo, "v_mul_lo_u32 %0, %0, %1")
 OP_KERNEL(k_ashr, "v_ashrrev_i32 %0, %1, %0")
 OP_KERNEL(k_permlane32, "v_permlane32_swap_b32 %0, %1")
 
+// 64-bit accumulator chains (the 32-bit-container LPC: i64 MACs, or exact f64 FMAs)
+#define OP_KERNEL64(NAME, T, ASM, CLOB)                                                           \
+    __global__ __launch_bounds__(64) void NAME(uint32_t* out, uint64_t* cyc, uint32_t seed) {     \
+        T a[8];                                                                                 \
+        for (int j = 0; j < 8; j++) a[j] = (T)(seed ^ (threadIdx.x * (j + 3)));                \
+        const uint32_t bi = seed | 1, ci = (seed >> 3) | 5;                                     \
+        const T bd = (T)bi, cd = (T)ci;                                                         \
+        (void)bd; (void)cd;                                                                     \
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();                                       \
+        const uint64_t r0 = __builtin_amdgcn_s_memrealtime();                                   \
+        for (int i = 0; i < ITER; i++) {                                                        \
+            for (int j = 0; j < 8; j++) asm volatile(ASM : "+v"(a[j]) : "v"(bi), "v"(ci), "v"(bd), "v"(cd) CLOB); \
+        }                                                                                       \
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();                                       \
+        const uint64_t r1 = __builtin_amdgcn_s_memrealtime();                                   \
+        uint64_t x = 0;                                                                         \
+        for (int j = 0; j < 8; j++) x ^= (uint64_t)a[j];                                        \
+        out[blockIdx.x * 64 + threadIdx.x] = (uint32_t)x;                                       \
+        if (threadIdx.x == 0) {                                                                 \
+            cyc[2 * blockIdx.x] = t1 - t0;                                                      \
+            cyc[2 * blockIdx.x + 1] = r1 - r0;                                                  \
+        }                                                                                       \
+    }
+OP_KERNEL64(k_mad_i64, uint64_t, "v_mad_i64_i32 %0, vcc, %1, %2, %0", : "vcc")
+OP_KERNEL64(k_fma_f64, double, "v_fma_f64 %0, %3, %4, %0", )
+
 typedef void (*KFn)(uint32_t*, uint64_t*, uint32_t);
 
 int main() {
@@ -61,7 +87,8 @@ int main() {
                          {"v_perm_b32", k_perm, 1},     {"v_lshl_or_b32", k_lshl_or, 1},
                          {"v_xad_u32", k_xad, 1},       {"v_dot2c_i32_i16", k_dot2c, 1},
                          {"v_pk_add_u16", k_pk_add, 1}, {"v_mul_lo_u32", k_mul_lo, 1},
-                         {"v_ashrrev_i32", k_ashr, 1},  {"v_permlane32_swap", k_permlane32, 1}};
+                         {"v_ashrrev_i32", k_ashr, 1},  {"v_permlane32_swap", k_permlane32, 1},
+                         {"v_mad_i64_i32", k_mad_i64, 1}, {"v_fma_f64", k_fma_f64, 1}};
     hipDeviceProp_t prop;
     hipGetDeviceProperties(&prop, 0);
     const int cus = prop.multiProcessorCount;
