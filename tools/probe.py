@@ -17,6 +17,15 @@ arg = sys.argv[1] if len(sys.argv) > 1 else "1250"
 if arg.isdigit():
     n = int(arg)
     streams = [s.flac for s in synth.generate_many([synth.config_c5(i) for i in range(n)])]
+elif arg.startswith("row:"):  # a row of tools/bench_configs.py (substring of its name)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_configs  # noqa: E402
+
+    name = next(k for k in bench_configs.ROWS if arg[4:] in k)
+    cfg, seg, frames, _ = bench_configs.ROWS[name]
+    st = synth.generate(**dict(cfg, n_samples=4096 * seg, seed=cfg.get("seed", 7)))
+    streams = [synth.tile_flac(st, max(1, frames // seg))]
+    n = name
 else:
     cfg = {"c2": synth.config_c2, "c3": synth.config_c3, "c4": synth.config_c4}[arg]()
     seg = 512

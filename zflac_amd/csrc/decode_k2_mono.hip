@@ -1,5 +1,6 @@
 // decode_k2_mono.hip -- decode kernel for SampleType container kind 2 (i32), mono layout.
 // One translation unit per (container, layout) so the instantiations compile in parallel.
+#define ZFLAC_RING_Q 32  // 128-word rings for 17..32 bits per sample (decode.inc)
 #include "decode.inc"
 
 namespace zflac {

@@ -1,5 +1,6 @@
 // decode_k2_stereo.hip -- decode kernel for SampleType container kind 2 (i32), stereo layout.
 // One translation unit per (container, layout) so the instantiations compile in parallel.
+#define ZFLAC_RING_Q 32  // 128-word rings for 17..32 bits per sample (decode.inc)
 #include "decode.inc"
 
 namespace zflac {

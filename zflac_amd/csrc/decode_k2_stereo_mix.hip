@@ -1,6 +1,7 @@
 // decode_k2_stereo_mix.hip -- the MIX decode kernels (waves with CONSTANT / VERBATIM lanes) for
 // SampleType container kind 2 (i32), stereo layout. Kept out of decode_k2_stereo.hip so the
 // pure kernels' code object is unchanged by them.
+#define ZFLAC_RING_Q 32  // 128-word rings for 17..32 bits per sample (decode.inc)
 #include "decode.inc"
 
 namespace zflac {
