@@ -56,10 +56,12 @@ METRIC = "Msamples/s decoded (bit-exact) + achieved HBM GB/s, 4096-blk stereo"
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_current.json")
 
 
-def pmc_traffic(prefix: str, lib_sha: str | None):
+def pmc_traffic(prefix: str, lib_sha: str | None, src_sha: str | None = None):
     """Corrected HBM bytes per step of the kernels named `prefix`* (the per-order-bucket
     k_decode launches, timed together) from the committed PMC summary, or None; `bytes` only
-    when the summary was taken on the library build being timed (same sha256)."""
+    when the summary was taken on the library build being timed: the same .so (sha256), or a
+    build of the same sources and flags (zflac_amd.build.source_fingerprint; hipcc output is
+    not bit-reproducible, so a rebuild of unchanged sources has another .so hash)."""
     try:
         with open(PMC_SUMMARY) as f:
             d = json.load(f)
@@ -70,9 +72,12 @@ def pmc_traffic(prefix: str, lib_sha: str | None):
         return None
     rd = sum(r["hbm_read_bytes"] for r in rows)
     wr = sum(r["hbm_write_bytes"] for r in rows)
-    same = lib_sha is not None and d.get("lib_sha256") == lib_sha
+    same_lib = lib_sha is not None and d.get("lib_sha256") == lib_sha
+    same_src = src_sha is not None and d.get("src_sha256") == src_sha
+    same = same_lib or same_src
     return {"bytes": int(rd + wr) if same else None, "read": int(rd), "write": int(wr), "kernels": len(rows),
-            "same_build": same, "lib_sha256": d.get("lib_sha256"),
+            "same_build": same, "match": "lib" if same_lib else ("sources" if same_src else None),
+            "lib_sha256": d.get("lib_sha256"), "src_sha256": d.get("src_sha256"),
             "source": os.path.relpath(d.get("_source", PMC_SUMMARY), ROOT)}
 
 
@@ -533,7 +538,10 @@ def main():
         alg_bytes = in_bytes + out_bytes  # per decode launch (this rank)
         achieved = alg_bytes / (dec_avg * 1e-3) / 1e9
         lib_sha = hashlib.sha256(open(zflac_amd.lib_path, "rb").read()).hexdigest()
-        pmc = pmc_traffic("zflac::k_decode<1, 2", lib_sha)
+        from zflac_amd import build as zbuild
+
+        src_sha = zbuild.source_fingerprint() if zbuild.sources_present() else None
+        pmc = pmc_traffic("zflac::k_decode<1, 2", lib_sha, src_sha)
         line = {
             "metric": METRIC,
             "value": round(value, 1),

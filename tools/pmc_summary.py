@@ -60,6 +60,13 @@ def main():
     out = {"calibration": {"fetch_factor_private_16B": f_read, "write_factor_private_16B": w_write,
                            "write_factor_runs_128B": w_runs},
            "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(), "_source": a.dir, "kernels": {}}
+    if not a.lib:  # the in-tree build: also its source fingerprint (builds are not bit-reproducible)
+        import sys
+
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from zflac_amd import build as zbuild
+
+        out["src_sha256"] = zbuild.source_fingerprint()
     runs = [d for d in sorted(glob.glob(os.path.join(a.dir, "p*"))) if os.path.isdir(d)]
     merged = defaultdict(dict)
     for d in runs:

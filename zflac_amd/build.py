@@ -16,6 +16,25 @@ SOURCES += [os.path.join(CSRC, n) for n in ("scan.hip", "md5.hip", "crc16.hip", 
 HEADERS = [os.path.join(CSRC, n) for n in ("common.h", "md5.hpp", "device_common.h", "decode.inc")]
 DEPS = SOURCES + HEADERS + [os.path.join(ROOT, "include", "zflac_hip.h")]
 ARCH = os.environ.get("ZFLAC_OFFLOAD_ARCH", "gfx950")
+CFLAGS = ["-O3", "-std=c++20", "-fPIC", "-Wall", "-Wno-unused-function"]
+
+
+def source_fingerprint() -> str:
+    """sha256 over the library's sources, headers, target and compile flags. hipcc output is
+    not bit-reproducible (each compile draws a new CUID), so this, not the .so's own hash, is
+    what says that two builds hold the same kernels (PMC summaries record it)."""
+    import hashlib
+
+    h = hashlib.sha256(f"{ARCH}|{' '.join(CFLAGS)}".encode())
+    for d in sorted(DEPS):
+        h.update(os.path.basename(d).encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def sources_present() -> bool:
+    return all(os.path.exists(d) for d in DEPS)
 
 
 def needs_build() -> bool:
@@ -49,8 +68,7 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
                                                                                for d in _obj_deps(src)):
             objs.append(obj)
             continue
-        cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-Wall",
-               "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+        cmd = ["hipcc", f"--offload-arch={ARCH}"] + CFLAGS + ["-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
         cmd[1:1] = [f"-D{d}" for d in defines]
         if src.endswith(".hip"):
             cmd[1:1] = ["-x", "hip"]
