@@ -185,71 +185,72 @@ __device__ __forceinline__ T wave_incl_sum(T v) {
 // ----------------------------------------------------------------------------------
 constexpr int SCANK_THREADS = 1024;
 constexpr int SCANK_WAVES = SCANK_THREADS / 64;
-constexpr int SCANK_PER = 16;  // chunks a thread loads at once
+constexpr int SCANK_T = 4;  // chunks per thread per tile (16 contiguous bytes of counts)
 
-// Thread t owns chunks [t * per, (t + 1) * per). Its counts are loaded SCANK_PER at a time
-// (independent loads: one memory latency per group, where a per-element load loop costs
-// one latency per chunk), summed, the per-thread sums scanned in each wave (shuffles) and
-// across the 16 wave totals (one barrier), and the offsets written on a second pass over the
-// range (one group for batches up to 16 Ki chunks = 512 MiB of input: kept in registers
-// between the passes).
+// The chunks are scanned in tiles of 4,096: thread t owns chunks 4t..4t+3 of the tile, so a
+// wave's loads and stores cover 1 KiB of counts (2 KiB of units) contiguously; per-thread
+// sums are scanned in each wave (shuffles) and across the 16 wave totals (one barrier), and
+// the tile's total carries into the next tile (the C5 shard: ~11k chunks, 3 tiles). (Round 2
+// and v30: contiguous per-thread ranges of ~11 chunks, i.e. 44-byte lane strides.)
 __global__ __launch_bounds__(SCANK_THREADS) void k_scan_chunks(const uint32_t* cnt, const unsigned long long* units,
                                                                uint32_t n, uint32_t* off,
                                                                unsigned long long* uoff, uint32_t* n_frames) {
     __shared__ uint32_t s_c[SCANK_WAVES];
     __shared__ unsigned long long s_u[SCANK_WAVES];
     const uint32_t t = threadIdx.x, wv = t >> 6;
-    const uint32_t per = (n + SCANK_THREADS - 1) / SCANK_THREADS;
-    const uint32_t lo = min(t * per, n), hi = min(lo + per, n);
-    uint32_t c[SCANK_PER];
-    unsigned long long u[SCANK_PER];
-    auto load = [&](uint32_t g) {
+    uint32_t carry_c = 0;
+    unsigned long long carry_u = 0;
+    for (uint32_t tb = 0; tb < n; tb += SCANK_THREADS * SCANK_T) {
+        const uint32_t i0 = tb + t * SCANK_T;
+        uint32_t c[SCANK_T];
+        unsigned long long u[SCANK_T];
+        uint32_t sc = 0;
+        unsigned long long su = 0;
 #pragma unroll
-        for (int i = 0; i < SCANK_PER; i++) {
-            const bool in = g + i < hi;
-            c[i] = in ? cnt[g + i] : 0u;
-            u[i] = in ? units[g + i] : 0ull;
-        }
-    };
-    uint32_t sc = 0;
-    unsigned long long su = 0;
-    for (uint32_t g = lo; g < hi; g += SCANK_PER) {
-        load(g);
-#pragma unroll
-        for (int i = 0; i < SCANK_PER; i++) {
+        for (int i = 0; i < SCANK_T; i++) {
+            const bool in = i0 + i < n;
+            c[i] = in ? cnt[i0 + i] : 0u;
+            u[i] = in ? units[i0 + i] : 0ull;
             sc += c[i];
             su += u[i];
         }
-    }
-    const uint32_t ic = wave_incl_sum(sc);
-    const unsigned long long iu = wave_incl_sum(su);
-    if ((t & 63u) == 63u) {
-        s_c[wv] = ic;
-        s_u[wv] = iu;
-    }
-    __syncthreads();
-    uint32_t rc = ic - sc;
-    unsigned long long ru = iu - su;
-    for (uint32_t w = 0; w < wv; w++) {  // the waves before this one (LDS broadcasts)
-        rc += s_c[w];
-        ru += s_u[w];
-    }
-    if (t == SCANK_THREADS - 1) {
-        off[n] = rc + sc;
-        uoff[n] = ru + su;
-        *n_frames = rc + sc;
-    }
-    for (uint32_t g = lo; g < hi; g += SCANK_PER) {
-        if (hi - lo > (uint32_t)SCANK_PER) load(g);  // one group: still in registers
+        const uint32_t ic = wave_incl_sum(sc);
+        const unsigned long long iu = wave_incl_sum(su);
+        if ((t & 63u) == 63u) {
+            s_c[wv] = ic;
+            s_u[wv] = iu;
+        }
+        __syncthreads();
+        uint32_t rc = carry_c + ic - sc;
+        unsigned long long ru = carry_u + iu - su;
+        uint32_t tc = 0;
+        unsigned long long tu = 0;
 #pragma unroll
-        for (int i = 0; i < SCANK_PER; i++) {
-            if (g + i < hi) {
-                off[g + i] = rc;
-                uoff[g + i] = ru;
+        for (uint32_t w = 0; w < (uint32_t)SCANK_WAVES; w++) {  // LDS broadcasts
+            if (w < wv) {
+                rc += s_c[w];
+                ru += s_u[w];
+            }
+            tc += s_c[w];
+            tu += s_u[w];
+        }
+#pragma unroll
+        for (int i = 0; i < SCANK_T; i++) {
+            if (i0 + i < n) {
+                off[i0 + i] = rc;
+                uoff[i0 + i] = ru;
             }
             rc += c[i];
             ru += u[i];
         }
+        carry_c += tc;
+        carry_u += tu;
+        __syncthreads();  // s_c / s_u are rewritten by the next tile
+    }
+    if (t == 0) {
+        off[n] = carry_c;
+        uoff[n] = carry_u;
+        *n_frames = carry_c;
     }
 }
 
