@@ -51,7 +51,7 @@ FRAMES_PER_STREAM = 32
 BLOCK = 4096
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak
 METRIC = "Msamples/s decoded (bit-exact) + achieved HBM GB/s, 4096-blk stereo"
-# PMC summary of the current k_decode build (tools/pmc.sh + tools/pmc_summary.py; FETCH_SIZE /
+# PMC summary of the current k_decode build (tools/gpu.sh pmc; FETCH_SIZE /
 # WRITE_SIZE corrected by the factors tools/calib_pmc.hip measures for this access pattern)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_current.json")
 
@@ -60,8 +60,9 @@ def pmc_traffic(prefix: str, lib_sha: str | None, src_sha: str | None = None):
     """Corrected HBM bytes per step of the kernels named `prefix`* (the per-order-bucket
     k_decode launches, timed together) from the committed PMC summary, or None; `bytes` only
     when the summary was taken on the library build being timed: the same .so (sha256), or a
-    build of the same sources and flags (zflac_amd.build.source_fingerprint; hipcc output is
-    not bit-reproducible, so a rebuild of unchanged sources has another .so hash)."""
+    build of the same sources, flags and defines (the fingerprint each build embeds, read from
+    the library this process loaded: zflac_hip_build_id; hipcc output is not bit-reproducible,
+    so a rebuild of unchanged sources has another .so hash)."""
     try:
         with open(PMC_SUMMARY) as f:
             d = json.load(f)
@@ -346,20 +347,43 @@ def md5_leg(args, streams, device: int, barrier=lambda: None):
 def start_md5_child(args):
     """Start the process that will run md5_leg (same rank, same shard) with GPU_MAX_HW_QUEUES
     set, so the headline's process keeps the runtime's defaults. Started before this process
-    touches the GPU (no fork / exec from a process with a GPU context); it generates its
-    shard, then waits on stdin until md5_leg_in_child tells it to start."""
+    touches the GPU (no fork / exec from a process with a GPU context). It does not generate
+    anything: it blocks on its stdin until md5_leg_in_child sends it this rank's shard. Per
+    rank that is two processes (this one and the child) and host_threads(world) host threads."""
     cmd = [sys.executable, os.path.abspath(__file__), "--md5-leg-child", "--steps", str(args.steps), "--warmup",
            str(args.warmup), "--streams-per-gpu", str(args.streams_per_gpu), "--md5-inflight", str(args.md5_inflight)]
     if args.same_device:
         cmd.append("--same-device")
+    if args.dry_run:
+        cmd.append("--dry-run")
     env = dict(os.environ, GPU_MAX_HW_QUEUES=str(args.md5_hw_queues))
-    return subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    return subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE)
 
 
-def md5_leg_in_child(proc):
-    """Let the child started by start_md5_child run its leg now; returns its dict (None on
-    failure)."""
-    out, _ = proc.communicate("go\n")
+def write_shard(f, streams) -> None:
+    """The shard as bytes: stream count, each length (u64 little-endian), then the streams."""
+    f.write(np.array([len(streams)] + [len(s) for s in streams], dtype="<u8").tobytes())
+    for s in streams:
+        f.write(s)
+    f.flush()
+
+
+def read_shard(f):
+    n = int(np.frombuffer(f.read(8), dtype="<u8")[0])
+    lens = np.frombuffer(f.read(8 * n), dtype="<u8") if n else []
+    return [f.read(int(x)) for x in lens]
+
+
+def md5_leg_in_child(proc, streams):
+    """Send the child started by start_md5_child this rank's shard and let it run its leg;
+    returns its dict (None on failure)."""
+    try:
+        write_shard(proc.stdin, streams)
+        proc.stdin.close()
+    except (BrokenPipeError, OSError):
+        pass
+    out = proc.stdout.read().decode()
+    proc.wait()
     if proc.returncode != 0 or not out.strip():
         return None
     return json.loads(out.strip().splitlines()[-1])
@@ -373,10 +397,11 @@ def main():
         sys.exit(launch(args.gpus))
     world = int(env_world or 1)
     if args.md5_leg_child:  # the decode+MD5 leg of this rank, in its own process (start_md5_child)
-        rank = int(os.environ.get("RANK", "0"))
         device = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
-        streams = make_shard(rank, world, args.streams_per_gpu)
-        if sys.stdin.readline().strip() != "go":
+        streams = read_shard(sys.stdin.buffer)  # the parent's shard, not a regenerated one
+        if args.dry_run:
+            print(json.dumps({"dry_run": True, "streams": len(streams), "pid": os.getpid(),
+                              "digest": hashlib.sha256(b"".join(streams)).hexdigest()[:16]}), flush=True)
             return
         print(json.dumps(md5_leg(args, streams, device)), flush=True)
         return
@@ -386,7 +411,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     device = 0 if args.same_device else local_rank
     backend = args.backend or ("gloo" if (args.dry_run or args.same_device) else "nccl")
-    md5_proc = None if (args.no_md5 or args.dry_run) else start_md5_child(args)
+    md5_proc = None if args.no_md5 else start_md5_child(args)
     dist = None
     if world > 1:
         import torch
@@ -420,19 +445,27 @@ def main():
         barrier_sync()
         el = time.perf_counter() - t0
         tot = aggregate(dist, coll_dev, el, samples, sum(len(s) for s in streams), samples * 2, 0)
-        shards = [None] * world
+        digest = hashlib.sha256(b"".join(streams)).hexdigest()[:16]
+        child = md5_leg_in_child(md5_proc, streams) if md5_proc is not None else None
+        # per rank: this process, its decode+MD5 child, and the host threads it may use
         rng = shard_range(rank, world, args.streams_per_gpu)
-        mine = [rng.start, rng.stop]
+        mine = {"rank": rank, "shard": [rng.start, rng.stop], "pid": os.getpid(), "processes": 1 + (child is not None),
+                "host_threads": host_threads(world),
+                "child_got_shard": bool(child and child["digest"] == digest and child["streams"] == len(streams))}
+        ranks = [None] * world
         if dist is not None:
-            dist.all_gather_object(shards, mine)
+            dist.all_gather_object(ranks, mine)
         else:
-            shards = [mine]
+            ranks = [mine]
         if rank == 0:
             print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "value": None,
                               "config": {"streams_total": args.streams_per_gpu * world,
                                          "parallelism": f"stream-shard x{world}"},
-                              "shards": shards, "samples_total": tot.samples, "backend": backend,
-                              "digest_rank0": hashlib.sha256(b"".join(streams)).hexdigest()[:16]}), flush=True)
+                              "shards": [r["shard"] for r in ranks], "ranks": ranks,
+                              "processes_total": sum(r["processes"] for r in ranks),
+                              "host_threads_total": sum(r["host_threads"] for r in ranks),
+                              "host_cores": host_cores()[0],
+                              "samples_total": tot.samples, "backend": backend, "digest_rank0": digest}), flush=True)
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -514,7 +547,7 @@ def main():
         batch.close()
         batch = None
         progress("verification done; decode+MD5 leg")
-        md5 = md5_leg_in_child(md5_proc)
+        md5 = md5_leg_in_child(md5_proc, streams)
         ok = ok and bool(md5 and md5.get("all_match"))
 
     cpu = None
@@ -538,9 +571,8 @@ def main():
         alg_bytes = in_bytes + out_bytes  # per decode launch (this rank)
         achieved = alg_bytes / (dec_avg * 1e-3) / 1e9
         lib_sha = hashlib.sha256(open(zflac_amd.lib_path, "rb").read()).hexdigest()
-        from zflac_amd import build as zbuild
-
-        src_sha = zbuild.source_fingerprint() if zbuild.sources_present() else None
+        bid = zflac_amd.build_id()  # embedded by the build: the sources of the loaded library
+        src_sha = bid[4:] if bid and bid.startswith("src=") else None
         pmc = pmc_traffic("zflac::k_decode<1, 2", lib_sha, src_sha)
         line = {
             "metric": METRIC,
@@ -577,6 +609,7 @@ def main():
                                      "decode": round(float(np.mean(rec_ov["decode_ms"])), 4)} if serial else None,
             "traffic_detail": pmc,
             "lib_sha256": lib_sha[:16],
+            "build_id": bid,
             "device_md5": md5,
             "cpu_baseline": cpu,
             "e2e_decode": e2e,

@@ -89,6 +89,11 @@ typedef struct zflac_timings {
     double read_ms;     /* last batch_read / read: D2H of the samples (+ MD5 overlapped) */
     double host_md5_ms; /* last batch_read / read: host STREAMINFO MD5 (overlapped with the D2H) */
     double crc16_ms;    /* k_crc16 of the last run (ZFLAC_FLAG_CHECK_CRC16 with ZFLAC_FLAG_TIMING), else 0 */
+    /* (ABI 4) synchronous `rest` decode launches of the last run: frame groups of a k_decode
+     * history bucket the batch's launch plan had not predicted; the bucket is then added to
+     * the plan, so a later run of the same batch has none */
+    uint32_t rest_launches;
+    uint32_t reserved0;
 } zflac_timings;
 
 typedef struct zflac_batch zflac_batch;
@@ -179,9 +184,14 @@ const char *zflac_hip_error_name(int code);
 int zflac_hip_device_count(void);
 /* Library build tag, e.g. "zflac_hip gfx950 r3". */
 const char *zflac_hip_version(void);
+/* Identity of the compiled library: "src=<sha256 of its sources, headers, target, flags and
+ * -D defines>" (zflac_amd/build.py source_fingerprint). hipcc output is not bit-reproducible,
+ * so this, not a hash of the .so, says which kernels a measurement ran. */
+const char *zflac_hip_build_id(void);
 /* ABI revision of this header; bumped whenever a struct or a signature changes.
- * 3: zflac_hip_batch_timings_ex, zflac_hip_abi_version; device MD5 pipelined into submit. */
-#define ZFLAC_HIP_ABI_VERSION 3
+ * 3: zflac_hip_batch_timings_ex, zflac_hip_abi_version; device MD5 pipelined into submit.
+ * 4: zflac_timings.rest_launches; zflac_hip_build_id. */
+#define ZFLAC_HIP_ABI_VERSION 4
 int zflac_hip_abi_version(void);
 
 #ifdef __cplusplus

@@ -73,12 +73,26 @@ def test_kernels_compiled_for_gfx950():
 
 
 def test_abi_version_and_timings_struct():
-    """ABI revision 3; zflac_hip_batch_timings_ex takes the caller's struct size, and the
+    """ABI revision 4; zflac_hip_batch_timings_ex takes the caller's struct size, and the
     legacy entry point writes only the first-version layout (scan_ms .. md5_ms)."""
     L = _lib.load()
-    assert L.zflac_hip_abi_version() == 3
+    assert L.zflac_hip_abi_version() == 4
     t = _lib.zflac_timings()
-    assert ctypes.sizeof(t) == 128
+    assert ctypes.sizeof(t) == 136
+    assert _lib.zflac_timings.rest_launches.offset == 128
     assert _lib.zflac_timings.plan_ms.offset == 80  # ZFLAC_TIMINGS_V1_SIZE
     assert L.zflac_hip_batch_timings_ex(None, ctypes.byref(t), ctypes.sizeof(t)) == 14
     assert L.zflac_hip_batch_timings(None, ctypes.byref(t)) == 14
+
+
+def test_build_id_names_the_sources():
+    """The library embeds the fingerprint of the sources it was built from (build.py), and
+    the loaded library reports the same string the file holds."""
+    from zflac_amd import build
+
+    L = _lib.load()
+    bid = L.zflac_hip_build_id().decode()
+    assert re.fullmatch(r"src=[0-9a-f]{64}", bid)
+    assert build.lib_build_id(_lib.lib_path) == bid
+    if _lib.lib_path == build.LIB and not build.needs_build():
+        assert bid == "src=" + build.source_fingerprint()

@@ -235,8 +235,9 @@ def test_large_single_stream(gpu_ready, cfg):
 
 def _spliced_order_change():
     """Frames 0-2 LPC order 8, frames 3-5 LPC order 32 (16-bit mid/side): the host predicts
-    the order-8 bucket from the first frame, so the order-32 frame groups run in a bucket
-    launch with the small grid (bucket_grid in decode.inc)."""
+    the order-8 bucket from the first frame, so the order-32 frame groups have no launch of
+    their own in the first run and are decoded by the synchronous `rest` launch
+    (enqueue_rest in host.cpp); the bucket then joins the batch's launch plan."""
     base = dict(channels=2, bps=16, stereo_mode=10, block_size=4096, n_samples=4096 * 6, partition_order=4)
     a = synth.generate(**dict(base, order=8, precision=12, seed=4100))
     b = synth.generate(**dict(base, order=32, precision=12, seed=4101))
@@ -253,6 +254,11 @@ def test_bucket_misprediction_still_decodes(gpu_ready):
     # a batch of many such streams: 6 x 70 frames, so several frame groups per bucket
     b = zflac_amd.Batch([data] * 70, timing=True)
     b.run()
+    assert b.timings().rest_launches == 1  # the unpredicted order-32 groups
+    for i in range(0, 70, 9):
+        np.testing.assert_array_equal(b.read(i).samples.values, r.samples)
+    b.run()  # learned: the order-32 bucket has its own launch now, no synchronous rest launch
+    assert b.timings().rest_launches == 0
     for i in range(0, 70, 9):
         np.testing.assert_array_equal(b.read(i).samples.values, r.samples)
     b.close()
@@ -351,8 +357,8 @@ def test_both_walks_mutants(gpu_ready, walk):
 
 
 def test_huge_stream_multi_pass_chunk_scan(gpu_ready):
-    """One 590 MB stream (C3, 65,536 frames, the SURVEY 8(d) size): 18 Ki scan chunks, more
-    than k_scan_chunks keeps in registers per thread (16 Ki), so its grouped second pass runs;
+    """One 590 MB stream (C3, 65,536 frames, the SURVEY 8(d) size): 18 Ki scan chunks, i.e.
+    five of k_scan_chunks' 4,096-chunk tiles, with the running sums carried from tile to tile;
     decode() verifies the STREAMINFO MD5 of the whole 1 GiB output."""
     st = synth.generate(**synth.config_c3(n_frames=1024))
     data = synth.tile_flac(st, 64)
@@ -360,3 +366,26 @@ def test_huge_stream_multi_pass_chunk_scan(gpu_ready):
     d = zflac_amd.decode(data)
     assert d.samples.values.size == st.pcm.size * 64
     np.testing.assert_array_equal(d.samples.values[: st.pcm.size], expected_samples(st))
+
+
+@pytest.mark.parametrize("chunks", [4097, 8193])
+def test_chunk_scan_tile_boundary(gpu_ready, chunks):
+    """k_scan_chunks carries its candidate and sample-unit sums from one 4,096-chunk tile to
+    the next: a batch whose scan chunks end just past one and two tiles, with streams before
+    and after the long one. A wrong carry misplaces frames, which the STREAMINFO MD5 of every
+    stream (checked by read) and the oracle comparison catch."""
+    st = synth.generate(**synth.config_c3(n_frames=64))
+    seg = len(st.flac) - int(st.frame_offsets[0])
+    big = synth.tile_flac(st, -(-(chunks * 32768) // seg))
+    small = [synth.generate(**synth.config_c5(i, n_frames=4)).flac for i in range(3)]
+    streams = [small[0], big, small[1], small[2]]
+    b = zflac_amd.Batch(streams)
+    b.run()
+    for i, data in enumerate(streams):
+        d = b.read(i, verify_md5=True)
+        if data is big:
+            assert d.samples.values.size == st.pcm.size * (-(-(chunks * 32768) // seg))
+            np.testing.assert_array_equal(d.samples.values[: st.pcm.size], expected_samples(st))
+        else:
+            np.testing.assert_array_equal(d.samples.values, oracle.decode(data).samples)
+    b.close()

@@ -1,4 +1,4 @@
-"""Summarise a same-box A/B (tools/ab.sh output dir) into one JSON: per library, each run's
+"""Summarise a same-box A/B (`tools/gpu.sh ab` output dir) into one JSON: per library, each run's
 value / ms_per_step / serial step / isolated stage times. Usage: ab_summary.py <dir> <out.json> [note]"""
 import glob
 import json

@@ -30,25 +30,27 @@ import synth  # noqa: E402
 import zflac_amd  # noqa: E402
 
 B = 4096
+SAT = 32768  # frames of the format rows
 ROWS = {
     # name: (flacgen config of one segment, segment frames, total frames, unknown total or
     # "bad_crc8")
     "C2 mono 16-bit fixed-2 k=4": (synth.config_c2(), 1024, 65536, False),
     "C3 stereo M/S 16-bit LPC-8": (synth.config_c3(), 1024, 65536, False),
     "C4 stereo 24-bit LPC-32 shift 15 wasted 4": (synth.config_c4(), 512, 65536, False),
-    "verbatim stereo 16-bit": (dict(channels=2, bps=16, predictor=0, stereo_mode=1, block_size=B), 256, 4096, False),
-    "constant-heavy stereo 16-bit": (dict(channels=2, bps=16, stereo_mode=1, silence_every=1, block_size=B), 256, 4096,
+    # format rows at a saturating size: 32,768 frames (512-1,024 decode waves)
+    "verbatim stereo 16-bit": (dict(channels=2, bps=16, predictor=0, stereo_mode=1, block_size=B), 256, SAT, False),
+    "constant-heavy stereo 16-bit": (dict(channels=2, bps=16, stereo_mode=1, silence_every=1, block_size=B), 256, SAT,
                                      False),
     "mono 8-bit LPC-4": (dict(channels=1, bps=8, order=4, precision=7, block_size=B, noise_lsb=1.0, tone_amp=0.3), 256,
-                         4096, False),
+                         SAT, False),
     "stereo 12-bit M/S LPC-8": (dict(channels=2, bps=12, stereo_mode=10, order=8, block_size=B, noise_lsb=4.0), 256,
-                                4096, False),
+                                SAT, False),
     "stereo 20-bit M/S LPC-12": (dict(channels=2, bps=20, stereo_mode=10, order=12, precision=14, block_size=B,
-                                      noise_lsb=16.0), 256, 4096, False),
+                                      noise_lsb=16.0), 256, SAT, False),
     "stereo 32-bit LPC-8": (dict(channels=2, bps=32, stereo_mode=1, order=8, precision=15, block_size=B, tone_amp=0.2,
-                                 noise_lsb=1e6), 256, 4096, False),
+                                 noise_lsb=1e6), 256, SAT, False),
     "6-channel 24-bit LPC-10": (dict(channels=6, bps=24, order=10, precision=14, block_size=B, noise_lsb=64.0), 128,
-                                2048, False),
+                                SAT, False),
     "C3, 2600 frames (a ~4-minute track)": (synth.config_c3(), 2600, 2600, False),
     "C3, total unknown (sequential planner)": (synth.config_c3(), 256, 4096, True),
     "C3, planted false syncs (repair path)": (dict(channels=2, bps=16, stereo_mode=1, order=8, block_size=B,

@@ -1,4 +1,4 @@
-"""Summarise a tools/pmc.sh run: per-kernel PMC counters per dispatch, FETCH/WRITE calibration
+"""Summarise a `tools/gpu.sh pmc` run: per-kernel PMC counters per dispatch, FETCH/WRITE calibration
 factors from tools/calib_pmc.hip, and the corrected HBM traffic of the decode kernel.
 
 Usage: python tools/pmc_summary.py gpurun_out/<tag> [--json out.json]
@@ -60,13 +60,15 @@ def main():
     out = {"calibration": {"fetch_factor_private_16B": f_read, "write_factor_private_16B": w_write,
                            "write_factor_runs_128B": w_runs},
            "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(), "_source": a.dir, "kernels": {}}
-    if not a.lib:  # the in-tree build: also its source fingerprint (builds are not bit-reproducible)
-        import sys
+    # the source fingerprint embedded in the measured library itself (builds are not
+    # bit-reproducible; bench.py matches the library it loads against this)
+    import sys
 
-        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        from zflac_amd import build as zbuild
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from zflac_amd import build as zbuild
 
-        out["src_sha256"] = zbuild.source_fingerprint()
+    bid = zbuild.lib_build_id(lib)
+    out["src_sha256"] = bid[4:] if bid else None
     runs = [d for d in sorted(glob.glob(os.path.join(a.dir, "p*"))) if os.path.isdir(d)]
     merged = defaultdict(dict)
     for d in runs:

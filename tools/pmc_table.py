@@ -1,4 +1,4 @@
-"""Print per-dispatch PMC counters of one kernel from pmc_passes.sh output dirs.
+"""Print per-dispatch PMC counters of one kernel from `tools/gpu.sh pmc` output dirs.
 Usage: python tools/pmc_table.py <kernel substring> gpurun_out/<tag> [gpurun_out/<tag2> ...]"""
 import csv, glob, os, sys
 from collections import defaultdict

@@ -16,6 +16,6 @@ from __future__ import annotations
 
 from . import errors
 from ._lib import lib_path
-from .api import Batch, DecodedFLAC, Samples, decode, decode_many, device_count
+from .api import Batch, DecodedFLAC, Samples, build_id, decode, decode_many, device_count
 
-__all__ = ["decode", "decode_many", "DecodedFLAC", "Samples", "Batch", "errors", "device_count", "lib_path"]
+__all__ = ["decode", "decode_many", "DecodedFLAC", "Samples", "Batch", "errors", "device_count", "build_id", "lib_path"]

@@ -66,6 +66,11 @@ def device_count() -> int:
     return _lib.load().zflac_hip_device_count()
 
 
+def build_id() -> str:
+    """"src=<fingerprint>" of the loaded library's sources (zflac_hip_build_id)."""
+    return _lib.load().zflac_hip_build_id().decode()
+
+
 def _aligned_empty(nbytes: int, dtype) -> np.ndarray:
     """32-byte aligned buffer, as zflac allocates its samples (src/zflac.zig:331)."""
     raw = np.empty(nbytes + 32, dtype=np.uint8)

@@ -19,13 +19,15 @@ ARCH = os.environ.get("ZFLAC_OFFLOAD_ARCH", "gfx950")
 CFLAGS = ["-O3", "-std=c++20", "-fPIC", "-Wall", "-Wno-unused-function"]
 
 
-def source_fingerprint() -> str:
-    """sha256 over the library's sources, headers, target and compile flags. hipcc output is
-    not bit-reproducible (each compile draws a new CUID), so this, not the .so's own hash, is
-    what says that two builds hold the same kernels (PMC summaries record it)."""
+def source_fingerprint(defines=()) -> str:
+    """sha256 over the library's sources, headers, target, compile flags and -D defines. hipcc
+    output is not bit-reproducible (each compile draws a new CUID), so this, not the .so's own
+    hash, is what says that two builds hold the same kernels. Every build embeds it
+    (zflac_hip_build_id() returns "src=<fingerprint>"), so a measurement names the kernels of
+    the library it actually loaded."""
     import hashlib
 
-    h = hashlib.sha256(f"{ARCH}|{' '.join(CFLAGS)}".encode())
+    h = hashlib.sha256(f"{ARCH}|{' '.join(CFLAGS)}|{' '.join(sorted(defines))}".encode())
     for d in sorted(DEPS):
         h.update(os.path.basename(d).encode())
         with open(d, "rb") as f:
@@ -44,8 +46,24 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in DEPS)
 
 
+def lib_build_id(path: str | None = None) -> str | None:
+    """The build id ("src=<fingerprint>") embedded in a built library, read from the .so file
+    without loading it (so it works without a GPU and for any ZFLAC_HIP_LIB variant)."""
+    import re
+
+    try:
+        with open(path or LIB, "rb") as f:
+            m = re.search(rb"src=([0-9a-f]{64})", f.read())
+    except OSError:
+        return None
+    return m.group(0).decode() if m else None
+
+
 def _obj_deps(src: str):
-    """Headers a translation unit includes (decode.inc only for the decode units)."""
+    """Headers a translation unit includes (decode.inc only for the decode units). host.cpp
+    embeds the fingerprint of every source, so it depends on all of them."""
+    if src.endswith("host.cpp"):
+        return list(DEPS)
     hdrs = [h for h in HEADERS if not h.endswith("decode.inc") or "decode_k" in src]
     return [src] + hdrs + [os.path.join(ROOT, "include", "zflac_hip.h")]
 
@@ -61,6 +79,7 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
     build_dir = os.path.join(HERE, "_build" + ("_" + tag if tag else ""))
     os.makedirs(build_dir, exist_ok=True)
     procs = []
+    fp = source_fingerprint(defines)
     jobs = max(1, min(int(os.environ.get("MAX_JOBS", "8")), os.cpu_count() or 1, 16))
     for src in SOURCES:  # translation units compile in parallel; up-to-date objects are kept
         obj = os.path.join(build_dir, os.path.basename(src) + ".o")
@@ -72,6 +91,8 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
         cmd[1:1] = [f"-D{d}" for d in defines]
         if src.endswith(".hip"):
             cmd[1:1] = ["-x", "hip"]
+        if src.endswith("host.cpp"):
+            cmd[1:1] = [f'-DZFLAC_BUILD_ID="src={fp}"']
         if verbose:
             print(" ".join(cmd))
         while sum(p.poll() is None for _, p in procs) >= jobs:  # bounded: each decode unit is GBs of RAM

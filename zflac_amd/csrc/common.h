@@ -154,6 +154,7 @@ constexpr uint32_t SPARSE_DECODE_BLOCKS = 256;
 __host__ __device__ inline constexpr uint32_t bucket_bit(uint32_t mb, bool mix) {
     return mix ? (mb <= 8 ? 16u : 32u) : (mb == 8 ? 1u : (mb == 4 ? 2u : (mb == 16 ? 4u : 8u)));
 }
+constexpr uint32_t BUCKET_MASK_ALL = 63u;
 
 // One stream for k_md5 (md5.hip): the message is the decoded samples before left-justify,
 // rebuilt from the justified device samples (src/zflac.zig:267-280).

@@ -301,6 +301,10 @@ struct Class {
     uint64_t in_bytes = 0, out_elems = 0;
     uint32_t cap = 0;
     uint64_t est_frames = 0;  // frames expected from the STREAMINFO totals (walk choice)
+    // frames the walk / decode grids are sized for (their loops stride over any excess): the
+    // exact frame count of fixed-blocking streams with a STREAMINFO total, plus slack; raised
+    // when a run finds more candidates (false syncs) than that
+    uint32_t grid_frames = 0;
     // decode launches given a full grid (DecodeArgs::full_mask): the buckets predicted from
     // the first subframe of each member's first frame, at batch creation (plan_buckets)
     uint32_t full_mask = 0;
@@ -483,9 +487,10 @@ void upload_streams(int device, uint8_t* dev, uint64_t total, const std::vector<
 }
 
 // The k_decode buckets (history size MB, MIX for constant / verbatim subframes) that get a
-// full grid: predicted from the first subframe of each member's first frame, whose type byte
-// follows the frame header (src/zflac.zig:426-429). k_decode classifies every frame group
-// itself; the prediction only sizes the launches (bucket_grid in decode.inc).
+// launch of their own: predicted from the first subframe of each member's first frame, whose
+// type byte follows the frame header (src/zflac.zig:426-429). k_decode classifies every frame
+// group itself (the order-8 launch); groups of a bucket without a launch are decoded by the
+// `rest` launch (enqueue_rest), after which the bucket is added to the mask (finish_batch).
 uint32_t plan_buckets(const zflac_batch* b, const Class& C, const zflac_stream* src) {
     uint32_t mask = bucket_bit(8, false);
     for (uint32_t i : C.members) {
@@ -513,7 +518,7 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     C.in_bytes = off;
     C.in.alloc(off + INPUT_PAD);
     uint64_t out = 0;
-    uint64_t est_frames = 0;
+    uint64_t est_frames = 0, grid_frames = 0;
     C.desc.resize(C.members.size());
     C.chunks.clear();
     for (size_t m = 0; m < C.members.size(); m++) {
@@ -553,7 +558,11 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
         D.end_chunk = (uint32_t)C.chunks.size();
         const uint64_t minb = std::max<uint64_t>(16, s.si.min_block ? s.si.min_block : 16);
         // (at most one candidate per two bytes: a huge STREAMINFO total cannot inflate it)
-        est_frames += std::min<uint64_t>(s.si.total ? s.si.total / minb : s.len / 16, s.len / 2) + 2;
+        const uint64_t est = std::min<uint64_t>(s.si.total ? s.si.total / minb : s.len / 16, s.len / 2) + 2;
+        est_frames += est;
+        // fixed blocking with a known total: zflac reads exactly ceil(total / block) frames (:341)
+        const bool fixed = s.si.min_block == s.si.max_block && s.si.min_block >= 16;
+        grid_frames += (s.si.total && fixed) ? (s.si.total + s.si.min_block - 1) / s.si.min_block : est;
     }
     C.out_elems = out;
     C.out.alloc(out * esz + 32);
@@ -586,6 +595,7 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     C.h_status = C.pin.p + 4;
     C.cap = (uint32_t)std::min<uint64_t>(est_frames + C.chunks.size() * 2 + 1024, 0x7FFFFFFFull);
     C.est_frames = est_frames;
+    C.grid_frames = (uint32_t)std::min<uint64_t>(grid_frames + grid_frames / 64 + 64, C.cap);
 }
 
 void alloc_candidates(Class& C) {
@@ -662,8 +672,8 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     DecodeArgs da = decode_args(C);
     da.bucket_used = C.misc.p + 2;
     da.full_mask = C.full_mask;
-    ck(launch_decode(C.kind, da, C.cap, b->stream, timing_last ? b->ev[4] : nullptr, b->front, b->front_join,
-                     C.est_frames, b->flags));
+    ck(launch_decode(C.kind, da, std::min(C.grid_frames, C.cap), b->stream, timing_last ? b->ev[4] : nullptr,
+                     b->front, b->front_join, C.est_frames, b->flags));
     st = b->stream;  // decode, verify and the read-backs
     if (timing_last) ck(hipEventRecord(b->ev[2], st));
     VerifyArgs va;
@@ -694,7 +704,7 @@ void enqueue_rest(zflac_batch* b, Class& C) {
     DecodeArgs da = decode_args(C);
     da.full_mask = C.full_mask;
     da.rest_only = 1;
-    ck(launch_decode(C.kind, da, C.cap, st));
+    ck(launch_decode(C.kind, da, std::min(C.grid_frames, C.cap), st));
     ck(hipMemsetAsync(C.status.p, 0, C.members.size() * sizeof(uint32_t), st));
     VerifyArgs va;
     va.streams = C.d_desc.p;
@@ -1013,19 +1023,28 @@ void finish_batch(zflac_batch* b) {
     ck(hipSetDevice(b->device));
     const bool timing = (b->flags & ZFLAC_FLAG_TIMING) != 0;
     ck(hipStreamSynchronize(b->stream));
+    uint32_t rest_launches = 0;
     for (size_t ci = 0; ci < b->classes.size(); ci++) {
         Class& C = *b->classes[ci];
         for (int attempt = 0; attempt < 3; attempt++) {
             if (!C.h_misc[1] && C.h_misc[0] <= C.cap) break;
             C.cap = std::max<uint32_t>(C.h_misc[0] + 1024, C.cap * 2);  // candidate table overflow: grow, redo
+            C.grid_frames = std::max(C.grid_frames, C.h_misc[0]);
             alloc_candidates(C);
             C.redone = true;
             enqueue_class(b, C, false, false);
             ck(hipStreamSynchronize(b->stream));
         }
+        // more candidates than the grids were sized for (false syncs): correct (the kernels
+        // stride over them), but slower; size the next run's grids for them
+        if (C.h_misc[0] > C.grid_frames) C.grid_frames = std::min(C.cap, C.h_misc[0] + C.h_misc[0] / 64 + 64);
         if (C.full_mask && (C.h_misc[2] & ~C.full_mask)) {  // a bucket without a launch was used
             enqueue_rest(b, C);
             C.redone = true;
+            rest_launches++;
+            // from now on that bucket gets a launch of its own: later runs keep the pipelined
+            // MD5 and skip the synchronous rest launch (launches are only ever added)
+            C.full_mask |= C.h_misc[2] & BUCKET_MASK_ALL;
         }
     }
     const bool crc = (b->flags & ZFLAC_FLAG_CHECK_CRC16) != 0;
@@ -1135,6 +1154,7 @@ void finish_batch(zflac_batch* b) {
     b->timings.input_bytes = in_bytes;
     b->timings.output_bytes = out_bytes;
     b->timings.samples = samples;
+    b->timings.rest_launches = rest_launches;
 }
 
 // MD5 of the decoded stream exactly as zflac hashes it: before left-justify, 24-bit
@@ -1472,7 +1492,12 @@ int zflac_hip_device_count(void) {
     return n;
 }
 
-const char* zflac_hip_version(void) { return "zflac_hip gfx950 r3"; }
+const char* zflac_hip_version(void) { return "zflac_hip gfx950 r4"; }
+
+#ifndef ZFLAC_BUILD_ID
+#define ZFLAC_BUILD_ID "unknown"
+#endif
+const char* zflac_hip_build_id(void) { return ZFLAC_BUILD_ID; }
 
 int zflac_hip_batch_create(const zflac_stream* streams, size_t n, int device, int flags, zflac_batch** out) {
     return create_batch(streams, n, device, flags, out);
