@@ -101,7 +101,11 @@ def parse_args():
     ap.add_argument("--md5-inflight", type=int, default=12, help="batches in flight in the decode+MD5 leg")
     ap.add_argument("--md5-hw-queues", type=int, default=16,
                     help="GPU_MAX_HW_QUEUES of the decode+MD5 leg's process (one HIP stream per batch in flight)")
+    ap.add_argument("--sched", choices=["rr", "ready"], default="rr",
+                    help="headline runs in flight: round robin, or whichever batch finished first")
     ap.add_argument("--md5-leg-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--md5-only", action="store_true",
+                    help="only the decode+MD5 leg, in this process (kernel traces: set GPU_MAX_HW_QUEUES outside)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the single-stream decode() legs")
     ap.add_argument("--e2e-frames", type=int, default=65536, help="frames of the long single stream")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default=None)
@@ -294,10 +298,37 @@ def e2e_leg(name: str, cfg: dict, seg_frames: int, frames: int, oracle_full: boo
             "md5_bound_msps": round(n / (tm["host_md5_ms"] * 1e-3) / 1e6, 1) if tm["host_md5_ms"] else None}
 
 
+def run_ready_order(batches, k: int, on_done=None) -> None:
+    """k runs over `batches`, one run in flight per batch: every batch is submitted, then
+    whichever batch's run has finished (zflac_hip_batch_ready) is collected and resubmitted
+    until k runs have been submitted, then the rest drain. Round robin instead waits for the
+    oldest run while younger ones may already be done (head-of-line blocking: with the
+    decode+MD5 leg's ~9 ms hashes, a slow batch idled the others)."""
+    pending = [False] * len(batches)
+    submitted = 0
+    for j, b in enumerate(batches):
+        if submitted == k:
+            break
+        b.submit()
+        pending[j] = True
+        submitted += 1
+    while any(pending):
+        for j, b in enumerate(batches):
+            if pending[j] and b.ready():
+                b.wait()
+                pending[j] = False
+                if on_done is not None:
+                    on_done(j)
+                if submitted < k:
+                    b.submit()
+                    pending[j] = True
+                    submitted += 1
+
+
 def md5_leg(args, streams, device: int, barrier=lambda: None):
     """decode + STREAMINFO MD5 of every stream of the shard: batches created with
     ZFLAC_FLAG_DEVICE_MD5, whose k_md5 zflac_hip_batch_submit enqueues right behind each
-    run's kernels; `md5_inflight` batches round robin, so one batch's hash (a serial chain
+    run's kernels; `md5_inflight` batches in completion order (run_ready_order), so one batch's hash (a serial chain
     per stream, ~7 ms for this shard) runs beside the other batches' runs."""
     import zflac_amd
 
@@ -305,22 +336,8 @@ def md5_leg(args, streams, device: int, barrier=lambda: None):
     mbs = [zflac_amd.Batch(streams, device=device, timing=True, device_md5=True) for _ in range(k_md5)]
     rec = []
 
-    def done(j):
-        mbs[j].wait()
-        rec.append(mbs[j].timings().md5_ms)
-
     def steps(k):
-        pending = [False] * len(mbs)
-        for i in range(k):
-            j = i % len(mbs)
-            if pending[j]:
-                done(j)
-            mbs[j].submit()
-            pending[j] = True
-        for t in range(len(mbs)):
-            j = (k + t) % len(mbs)
-            if pending[j]:
-                done(j)
+        run_ready_order(mbs, k, lambda j: rec.append(mbs[j].timings().md5_ms))
 
     steps(max(args.warmup, k_md5))
     rec.clear()
@@ -404,6 +421,11 @@ def main():
                               "digest": hashlib.sha256(b"".join(streams)).hexdigest()[:16]}), flush=True)
             return
         print(json.dumps(md5_leg(args, streams, device)), flush=True)
+        return
+    if args.md5_only:  # the decode+MD5 leg alone, in this process (tools/gpu.sh md5trace)
+        rank = int(os.environ.get("RANK", "0"))
+        device = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
+        print(json.dumps(md5_leg(args, make_shard(rank, world, args.streams_per_gpu), device)), flush=True)
         return
     if args.gpus is not None and args.gpus != world:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
@@ -492,6 +514,14 @@ def main():
                 for name in STAGES:
                     rec[name].append(getattr(t, name))
 
+        if args.sched == "ready":
+            def rec_done(j):
+                if rec is not None:
+                    t = bs[j].timings()
+                    for name in STAGES:
+                        rec[name].append(getattr(t, name))
+            run_ready_order(bs, k, rec_done)
+            return
         for i in range(k):
             j = i % len(bs)
             if pending[j]:

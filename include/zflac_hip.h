@@ -132,6 +132,11 @@ int zflac_hip_batch_run(zflac_batch *b);
  * for its kernels. */
 int zflac_hip_batch_submit(zflac_batch *b);
 int zflac_hip_batch_wait(zflac_batch *b);
+/* (ABI 4) Non-blocking: 1 when the device work of the submitted run has finished (so
+ * _wait returns without waiting on the GPU), 0 while it runs, -ZFLAC_E_INVALID_ARGUMENT
+ * without a submitted run, -ZFLAC_E_DEVICE on a device error. A caller with several batches
+ * in flight waits for whichever is ready instead of the oldest. */
+int zflac_hip_batch_ready(zflac_batch *b);
 /* Per-stream result of the last run: zflac error code, and shape when OK.
  * Before the first completed run: ZFLAC_E_INVALID_ARGUMENT (as for _read, _md5 and
  * _device_samples, which returns NULL). */
@@ -190,7 +195,7 @@ const char *zflac_hip_version(void);
 const char *zflac_hip_build_id(void);
 /* ABI revision of this header; bumped whenever a struct or a signature changes.
  * 3: zflac_hip_batch_timings_ex, zflac_hip_abi_version; device MD5 pipelined into submit.
- * 4: zflac_timings.rest_launches; zflac_hip_build_id. */
+ * 4: zflac_timings.rest_launches; zflac_hip_build_id; zflac_hip_batch_ready. */
 #define ZFLAC_HIP_ABI_VERSION 4
 int zflac_hip_abi_version(void);
 

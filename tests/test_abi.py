@@ -59,6 +59,7 @@ def test_invalid_arguments():
     assert L.zflac_hip_batch_run(None) == 14
     assert L.zflac_hip_batch_submit(None) == 14
     assert L.zflac_hip_batch_wait(None) == 14
+    assert L.zflac_hip_batch_ready(None) == -14
     assert L.zflac_hip_batch_info(None, 0, None) == 14
     assert L.zflac_hip_batch_read(None, 0, None, 0, 0) == 14
     assert L.zflac_hip_batch_size(None) == 0

@@ -208,6 +208,34 @@ def test_overlapped_batches_submit_wait(gpu_ready):
         b.close()  # the in-flight one waits for its kernels first
 
 
+def test_batch_ready_completion_order(gpu_ready):
+    """zflac_hip_batch_ready: InvalidArgument without a submitted run; after submit it turns
+    true once the run's device work is done (then _wait only produces the results), so a
+    caller can collect whichever of several batches finished first (bench.run_ready_order)."""
+    import time
+
+    c5 = [s.flac for s in synth.generate_many([synth.config_c5(i, n_frames=8) for i in range(40)])]
+    bs = [zflac_amd.Batch(c5[k::2], device_md5=k == 1) for k in range(2)]
+    with pytest.raises(errors.InvalidArgument):
+        bs[0].ready()
+    for rnd in range(3):
+        for b in bs:
+            b.submit()
+        left = set(range(len(bs)))
+        t0 = time.time()
+        while left:
+            for j in list(left):
+                if bs[j].ready():
+                    bs[j].wait()
+                    left.discard(j)
+            assert time.time() - t0 < 60
+        for k, b in enumerate(bs):
+            for i in range(0, len(b), 5):
+                np.testing.assert_array_equal(b.read(i).samples.values, oracle.decode(c5[2 * i + k], "fast").samples)
+    for b in bs:
+        b.close()
+
+
 def test_c5_shard_md5_property(gpu_ready):
     """Full-shape C5 members (32 frames each) at a reduced stream count: every stream's
     decoded PCM must hash to its STREAMINFO MD5 (checked inside read) and a sample of

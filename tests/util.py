@@ -67,6 +67,14 @@ PARITY_CONFIGS = {
     "auto_stereo_lpc12": dict(channels=2, bps=16, stereo_mode=-1, order=12, precision=14, block_size=4608,
                               n_samples=4608 * 3 + 17, partition_order=3),
     "mono8_lpc3": dict(channels=1, bps=8, order=3, precision=7, block_size=576, n_samples=576 * 9 + 3),
+    # 8-bit containers on the packed fast path (bytes four to a dword, 16-byte stores; stereo
+    # interleaved after permlane32_swap), 4096-sample frames and a short last frame
+    "mono8_lpc4_packed": dict(channels=1, bps=8, order=4, precision=7, block_size=4096, n_samples=4096 * 3 + 21,
+                              noise_lsb=1.0, tone_amp=0.3, wasted_bits=1),
+    "stereo8_ms_packed": dict(channels=2, bps=8, stereo_mode=10, order=4, precision=7, block_size=4096,
+                              n_samples=4096 * 3 + 5, noise_lsb=1.0, tone_amp=0.3),
+    "stereo8_ls_packed": dict(channels=2, bps=8, stereo_mode=8, order=6, precision=7, block_size=2048,
+                              n_samples=2048 * 4, noise_lsb=2.0, tone_amp=0.25),
     "stereo12_ms": dict(channels=2, bps=12, stereo_mode=10, order=4, block_size=1024, n_samples=1024 * 6),
     "ms20_lpc16_escape": dict(channels=2, bps=20, stereo_mode=10, order=16, precision=14, block_size=4096,
                               n_samples=4096 * 3, escape_every=7),

@@ -47,6 +47,7 @@ SIGNATURES = {
     "zflac_hip_batch_run": (ctypes.c_int, [_P]),
     "zflac_hip_batch_submit": (ctypes.c_int, [_P]),
     "zflac_hip_batch_wait": (ctypes.c_int, [_P]),
+    "zflac_hip_batch_ready": (ctypes.c_int, [_P]),
     "zflac_hip_batch_info": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(zflac_info)]),
     "zflac_hip_batch_read": (ctypes.c_int, [_P, ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.c_int]),
     "zflac_hip_batch_md5": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_char_p]),

@@ -144,6 +144,13 @@ class Batch:
     def wait(self) -> None:
         errors.check(self._L.zflac_hip_batch_wait(self._h), "batch_wait")
 
+    def ready(self) -> bool:
+        """The submitted run's device work has finished (zflac_hip_batch_ready, non-blocking)."""
+        rc = self._L.zflac_hip_batch_ready(self._h)
+        if rc < 0:
+            errors.check(-rc, "batch_ready")
+        return rc == 1
+
     def info(self, i: int):
         inf = _lib.zflac_info()
         rc = self._L.zflac_hip_batch_info(self._h, i, ctypes.byref(inf))

@@ -68,12 +68,17 @@ def _obj_deps(src: str):
     return [src] + hdrs + [os.path.join(ROOT, "include", "zflac_hip.h")]
 
 
-def build(force: bool = False, verbose: bool = False, defines=(), out: str | None = None) -> str:
+def build(force: bool = False, verbose: bool = False, defines=(), out: str | None = None, units=None) -> str:
     """Build libzflac_hip.so (or, with `out`, a variant with extra -D `defines` for timing
-    experiments: separate object directory, never the product library)."""
+    experiments: separate object directory, never the product library). `units`: basenames
+    of the translation units the defines affect; the variant takes every other unit's object
+    from the product build (built first), so a one-kernel experiment compiles one unit."""
     lib = out or LIB
     if not force and not defines and not out and not needs_build():
         return LIB
+    if units:
+        build()  # the product objects the variant shares
+        units = set(units) | {"host.cpp"}  # host.cpp embeds the variant's fingerprint
     objs = []
     tag = "_".join(d.replace("=", "-") for d in defines)
     build_dir = os.path.join(HERE, "_build" + ("_" + tag if tag else ""))
@@ -82,6 +87,9 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
     fp = source_fingerprint(defines)
     jobs = max(1, min(int(os.environ.get("MAX_JOBS", "8")), os.cpu_count() or 1, 16))
     for src in SOURCES:  # translation units compile in parallel; up-to-date objects are kept
+        if units and os.path.basename(src) not in units:
+            objs.append(os.path.join(HERE, "_build", os.path.basename(src) + ".o"))
+            continue
         obj = os.path.join(build_dir, os.path.basename(src) + ".o")
         if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d)
                                                                                for d in _obj_deps(src)):
@@ -109,7 +117,8 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
 
 
 if __name__ == "__main__":
-    # python -m zflac_amd.build [--force] [-DNAME ...] [-o out.so]
+    # python -m zflac_amd.build [--force] [-DNAME ...] [-o out.so] [--units a.hip,b.hip]
     a = sys.argv[1:]
     out = a[a.index("-o") + 1] if "-o" in a else None
-    build(force="--force" in a, verbose=True, defines=[x[2:] for x in a if x.startswith("-D")], out=out)
+    units = a[a.index("--units") + 1].split(",") if "--units" in a else None
+    build(force="--force" in a, verbose=True, defines=[x[2:] for x in a if x.startswith("-D")], out=out, units=units)

@@ -40,10 +40,12 @@ ZFLAC_DECL_LAUNCH(2)
 hipError_t launch_walk_wave(int kind, const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
 
 // Which subframe-start walk a launch over `frames` frames of `nch` channels uses: k_walk
-// (lane per frame: 64 serial chains per wave) needs tens of thousands of frames to fill the
-// chip; k_walk_wave (wave per frame, wave-wide bit scan of each Rice partition) fills it with
-// a few thousand, and walks the nch - 1 leading subframes of 3..8-channel frames with a
-// short chain each. ZFLAC_WALK=lane / wave forces one (timing experiments).
+// (lane per frame: 64 serial chains per wave, nch - 1 subframes each) needs tens of thousands
+// of subframe walks to fill the chip; k_walk_wave (wave per frame, wave-wide bit scan of each
+// Rice partition) fills it with a few thousand, at several times the instructions per code.
+// So the wave walk below WAVE_WALK_MAX_FRAMES subframe walks, the lane walk above, for every
+// channel count (a 32,768-frame 6-channel stream: lane walk).
+// ZFLAC_WALK=lane / wave forces one (timing experiments).
 static bool use_wave_walk(uint64_t frames, int nch, int flags) {
     static const int forced = [] {
         const char* e = std::getenv("ZFLAC_WALK");
@@ -52,7 +54,7 @@ static bool use_wave_walk(uint64_t frames, int nch, int flags) {
     if (flags & ZFLAC_FLAG_WALK_WAVE) return true;
     if (flags & ZFLAC_FLAG_WALK_LANE) return false;
     if (forced) return forced == 1;
-    return nch > 2 || frames * (uint64_t)(nch - 1) < WAVE_WALK_MAX_FRAMES;
+    return frames * (uint64_t)(nch - 1) < WAVE_WALK_MAX_FRAMES;
 }
 
 // k_walk or k_walk_wave (subframe start offsets, 2+ channels) then k_decode; `mid`
@@ -352,6 +354,7 @@ struct zflac_batch {
     std::vector<zflac::StreamState> streams;
     std::vector<std::unique_ptr<zflac::Class>> classes;
     hipEvent_t ev[10] = {};
+    hipEvent_t ev_done = nullptr;  // recorded behind the last work _submit enqueued (_ready)
     bool have_timing = false;
     bool ran = false;        // results exist only after a completed batch_run / batch_wait
     bool submitted = false;  // batch_submit enqueued a run that batch_wait has not finished
@@ -373,6 +376,7 @@ struct zflac_batch {
         for (auto& s : streams) s.override_out.reset();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
+        if (ev_done) (void)hipEventDestroy(ev_done);
         if (pipe_pin) (void)hipHostFree(pipe_pin);
         if (stream) (void)hipStreamDestroy(stream);
         if (front) (void)hipStreamDestroy(front);
@@ -1014,6 +1018,7 @@ void submit_batch(zflac_batch* b) {
         if (timing) ck(hipEventRecord(b->ev[9], b->stream));
         ck(hipMemcpyAsync(b->pipe_pin, b->pipe_dig.p, (size_t)n * 16, hipMemcpyDeviceToHost, b->stream));
     }
+    ck(hipEventRecord(b->ev_done, b->stream));  // zflac_hip_batch_ready
 }
 
 // Phase 2: wait for the pipeline, redo a class whose candidate table overflowed (grown,
@@ -1407,6 +1412,7 @@ int create_batch(const zflac_stream* streams, size_t n, int device, int flags, z
         // timing-only events: no system-scope fence (cache writeback + invalidate) at each
         // record, which would otherwise slow the kernel after it
         for (auto& e : b->ev) ck(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+        ck(hipEventCreateWithFlags(&b->ev_done, hipEventDisableTiming));
         const double t0 = now_ms();
         b->streams.resize(n);
         for (size_t i = 0; i < n; i++) {
@@ -1547,6 +1553,14 @@ int zflac_hip_batch_wait(zflac_batch* b) {
         return E_DEVICE;
     }
     return E_OK;
+}
+
+int zflac_hip_batch_ready(zflac_batch* b) {
+    if (!b || !b->submitted) return -E_INVALID_ARGUMENT;
+    const hipError_t e = hipEventQuery(b->ev_done);
+    if (e == hipSuccess) return 1;
+    if (e == hipErrorNotReady) return 0;
+    return -E_DEVICE;
 }
 
 int zflac_hip_batch_run(zflac_batch* b) {

@@ -25,10 +25,13 @@ namespace {
 
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) { return __builtin_amdgcn_alignbit(x, x, 32 - s); }
 
-#define MD_F(x, y, z) ((z) ^ ((x) & ((y) ^ (z))))
-#define MD_G(x, y, z) ((y) ^ ((z) & ((x) ^ (y))))
-#define MD_H(x, y, z) ((x) ^ (y) ^ (z))
-#define MD_I(x, y, z) ((y) ^ ((x) | ~(z)))
+// The round functions as single v_bitop3_b32 (gfx950): truth tables over x = 0xF0,
+// y = 0xCC, z = 0xAA. F = (x & y) | (~x & z), G = (x & z) | (y & ~z), H = x ^ y ^ z,
+// I = y ^ (x | ~z) (RFC 1321 3.4). Left to the compiler, H took two v_xor per round.
+#define MD_F(x, y, z) __builtin_amdgcn_bitop3_b32((x), (y), (z), 0xCA)
+#define MD_G(x, y, z) __builtin_amdgcn_bitop3_b32((x), (y), (z), 0xE4)
+#define MD_H(x, y, z) __builtin_amdgcn_bitop3_b32((x), (y), (z), 0x96)
+#define MD_I(x, y, z) __builtin_amdgcn_bitop3_b32((x), (y), (z), 0x39)
 #define MD_R(f, a, b, c, d, k, t, s) a = (b) + rotl((a) + f(b, c, d) + m[k] + (t), s)
 
 __device__ __forceinline__ void compress(uint32_t st[4], const uint32_t m[16]) {
@@ -191,6 +194,11 @@ __global__ __launch_bounds__(64) void k_md5(const Md5Job* __restrict__ jobs, uin
                                             uint32_t* __restrict__ digests) {
     const uint32_t t = blockIdx.x * 64 + threadIdx.x;
     if (t >= n_jobs) return;
+#ifdef ZFLAC_MD5_PRIO
+    // (experiment) the hash waves ahead of the decode waves they share SIMDs with: the
+    // serial chains then run at the pace of a wave alone, but the decode waves slow down
+    __builtin_amdgcn_s_setprio(ZFLAC_MD5_PRIO);
+#endif
     const Md5Job j = jobs[t];
     uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
     if (j.status && *j.status) {  // not certified by this run: the host hashes it after the planner
