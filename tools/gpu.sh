@@ -61,7 +61,7 @@ case $CMD in
         > $O/$NAME.json 2> $O/$NAME.err
     ;;
   md5trace)
-    export GPU_MAX_HW_QUEUES=16  # as the bench's decode+MD5 child runs (set before rocprofv3, not via env)
+    export GPU_MAX_HW_QUEUES=${MD5Q:-16}  # as the bench's decode+MD5 child runs (set before rocprofv3, not via env)
     prof $O/md5leg python3 $R/bench.py --md5-only --steps 24 --warmup 12 "$@" > $O/md5leg.log 2>&1
     ;;
   pmc)

@@ -149,12 +149,13 @@ struct DecodeArgs {
 constexpr uint32_t SPARSE_DECODE_BLOCKS = 256;
 
 // Bit of a k_decode launch (history bucket MB, MIX kernels) in DecodeArgs::bucket_used /
-// full_mask: 8 -> 1, 4 -> 2, 16 -> 4, 32 -> 8, MIX 8 -> 16, MIX 32 -> 32. The order-8 launch
+// full_mask: 8 -> 1, 4 -> 2, 16 -> 4, 32 -> 8, MIX 8 -> 16, MIX 32 -> 32, 12 -> 64. The order-8 launch
 // always runs (it classifies every wave).
 __host__ __device__ inline constexpr uint32_t bucket_bit(uint32_t mb, bool mix) {
-    return mix ? (mb <= 8 ? 16u : 32u) : (mb == 8 ? 1u : (mb == 4 ? 2u : (mb == 16 ? 4u : 8u)));
+    return mix ? (mb <= 8 ? 16u : 32u)
+               : (mb == 8 ? 1u : (mb == 4 ? 2u : (mb == 16 ? 4u : (mb == 12 ? 64u : 8u))));
 }
-constexpr uint32_t BUCKET_MASK_ALL = 63u;
+constexpr uint32_t BUCKET_MASK_ALL = 127u;
 
 // One stream for k_md5 (md5.hip): the message is the decoded samples before left-justify,
 // rebuilt from the justified device samples (src/zflac.zig:267-280).
@@ -174,6 +175,16 @@ struct Md5Job {
     uint32_t pad_;
     const uint32_t* status;  // optional: the stream's k_verify status; nonzero = not certified by
                              // this run (the sequential planner decodes it later), no hash
+};
+
+// Jobs of several runs for one k_md5_multi launch (the md5 hub, host.cpp): segment s is
+// jobs[s][0 .. start[s+1] - start[s]), its digests go to dig[s].
+constexpr int MD5_MAX_SEGS = 16;
+struct Md5Segs {
+    const Md5Job* jobs[MD5_MAX_SEGS];
+    uint32_t* dig[MD5_MAX_SEGS];
+    uint32_t start[MD5_MAX_SEGS + 1];
+    uint32_t nseg;
 };
 
 struct VerifyArgs {

@@ -100,6 +100,7 @@ hipError_t launch_verify(const VerifyArgs& a, uint32_t max_items, hipStream_t st
 hipError_t launch_crc16(const Crc16Args& a, uint32_t max_frames, hipStream_t st);
 hipError_t launch_sync_list(const SyncListArgs& a, hipStream_t st);
 hipError_t launch_md5(const Md5Job* jobs, uint32_t n_jobs, uint32_t* digests, hipStream_t st);
+hipError_t launch_md5_multi(const Md5Segs& sg, hipStream_t st);
 
 namespace {
 
@@ -340,6 +341,7 @@ struct Class {
 // ---------------------------------------------------------------------------------
 // Batch
 // ---------------------------------------------------------------------------------
+void hub_release_ext(zflac_batch* b);  // flush a run still pending in its device's md5 hub
 }  // namespace zflac
 
 struct zflac_batch {
@@ -355,6 +357,16 @@ struct zflac_batch {
     std::vector<std::unique_ptr<zflac::Class>> classes;
     hipEvent_t ev[10] = {};
     hipEvent_t ev_done = nullptr;  // recorded behind the last work _submit enqueued (_ready)
+    // the HIP stream of the run in flight: one of the device's run streams (DeviceStreams),
+    // so that many batches in flight share a few hardware queues; `stream` (the batch's own)
+    // carries the synchronous work (upload, regrowth, the sequential planner, read-backs)
+    hipStream_t rs = nullptr;
+    // ZFLAC_FLAG_DEVICE_MD5 runs hash in the device's md5 hub (one k_md5_multi launch over
+    // the runs of several batches, on the hub's stream): ev_done then marks the decode only,
+    // ev_md5 the hash and its digest read-back; md5_pending until the hub launched it
+    hipEvent_t ev_md5 = nullptr;
+    bool md5_pending = false;
+    bool md5_hub = false;  // this run's hash goes through the hub
     bool have_timing = false;
     bool ran = false;        // results exist only after a completed batch_run / batch_wait
     bool submitted = false;  // batch_submit enqueued a run that batch_wait has not finished
@@ -371,12 +383,21 @@ struct zflac_batch {
     zflac_timings timings = {};
     ~zflac_batch() {
         if (stream) (void)hipStreamSynchronize(stream);  // a submitted run may still use the buffers
+        if (ev_done) (void)hipEventSynchronize(ev_done);  // ... on its run stream
+        if (md5_pending) {  // still in the md5 hub: flush it, then let the hash finish
+            try {
+                zflac::hub_release_ext(this);
+            } catch (...) {
+            }
+        }
+        if (md5_hub && ev_md5) (void)hipEventSynchronize(ev_md5);
         if (front) (void)hipStreamSynchronize(front);
         classes.clear();
         for (auto& s : streams) s.override_out.reset();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (ev_done) (void)hipEventDestroy(ev_done);
+        if (ev_md5) (void)hipEventDestroy(ev_md5);
         if (pipe_pin) (void)hipHostFree(pipe_pin);
         if (stream) (void)hipStreamDestroy(stream);
         if (front) (void)hipStreamDestroy(front);
@@ -442,6 +463,25 @@ Uploader& uploader(int device) {
     return *u;
 }
 
+// The device's run streams: every batch run (zflac_hip_batch_submit) goes to the next one
+// in turn, so any number of batches in flight use n_run (3) hardware queues (runs on one
+// stream execute in submit order; three in flight is where the C5 shard's throughput peaks).
+// Created before any batch's own stream, so that with HIP's default four hardware queues
+// (GPU_MAX_HW_QUEUES) the three run streams and the md5 hub stream each hold one of their own.
+// ZFLAC_RUN_STREAMS / ZFLAC_HUB_STREAMS override the counts (at most 8 / 4).
+constexpr int MAX_RUN_STREAMS = 8;
+struct Md5Hub;
+struct DeviceStreams {
+    std::mutex mu;
+    hipStream_t run[MAX_RUN_STREAMS] = {};
+    uint32_t n_run = 3, next = 0;
+    std::unique_ptr<Md5Hub> hub_p;
+    Md5Hub& hub;
+    DeviceStreams();
+};
+
+DeviceStreams& device_streams(int device);
+
 // bytes [a, b) of the layout into dst
 void fill_window(uint8_t* dst, uint64_t a, uint64_t b, const std::vector<uint64_t>& in_off,
                  const std::vector<const uint8_t*>& srcs, const std::vector<uint64_t>& lens) {
@@ -504,7 +544,7 @@ uint32_t plan_buckets(const zflac_batch* b, const Class& C, const zflac_stream* 
         const uint32_t t = (src[i].data[p] >> 1) & 63;
         const uint32_t ord = t >= 32 ? t - 31 : (t >= 8 && t <= 12 ? t - 8 : 0);
         if (t <= 1) mask |= bucket_bit(8, true) | bucket_bit(32, true);  // the wave's order is unknown
-        else mask |= bucket_bit(ord <= 4 ? 4 : ord <= 8 ? 8 : ord <= 16 ? 16 : 32, false);
+        else mask |= bucket_bit(ord <= 4 ? 4 : ord <= 8 ? 8 : ord <= 12 ? 12 : ord <= 16 ? 16 : 32, false);
     }
     return mask;
 }
@@ -640,7 +680,7 @@ DecodeArgs decode_args(Class& C) {
 
 // Launch the whole parallel pipeline of one class on the batch stream.
 void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last) {
-    hipStream_t st = b->front ? b->front : b->stream;  // scan, compact (and the walk) there
+    hipStream_t st = b->front ? b->front : b->rs;  // scan, compact (and the walk) there
     const uint32_t nch = (uint32_t)C.chunks.size();
     ck(hipMemsetAsync(C.status.p, 0, C.members.size() * sizeof(uint32_t), st));
     ck(hipMemsetAsync(C.misc.p, 0, 4 * sizeof(uint32_t), st));
@@ -676,9 +716,9 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     DecodeArgs da = decode_args(C);
     da.bucket_used = C.misc.p + 2;
     da.full_mask = C.full_mask;
-    ck(launch_decode(C.kind, da, std::min(C.grid_frames, C.cap), b->stream, timing_last ? b->ev[4] : nullptr,
+    ck(launch_decode(C.kind, da, std::min(C.grid_frames, C.cap), b->rs, timing_last ? b->ev[4] : nullptr,
                      b->front, b->front_join, C.est_frames, b->flags));
-    st = b->stream;  // decode, verify and the read-backs
+    st = b->rs;  // decode, verify and the read-backs
     if (timing_last) ck(hipEventRecord(b->ev[2], st));
     VerifyArgs va;
     va.streams = C.d_desc.p;
@@ -999,26 +1039,126 @@ void finish_stream_sequential(zflac_batch* b, Class& C, uint32_t slot, const std
 void run_md5_device(zflac_batch* b, const std::vector<uint32_t>& which, bool timing);
 void finish_md5(zflac_batch* b, bool timing);
 
-// Phase 1 of a run: every class's parallel pipeline on the batch's stream, no host wait.
-// Two batches submitted back to back overlap on the device (each has its own stream and
-// buffers): the scan and walk of one run beside the decode of the other.
+// ---------------------------------------------------------------------------------
+// md5 hub: one per device. MD5 is one serial chain per stream (~8 ms for a C5 stream of
+// 32 frames), so a run's hash lasts as long as its longest chain whatever its lane count.
+// Hashing each run on its own batch stream made the decode+MD5 throughput the number of
+// batches in flight over (decode + hash latency), and each batch held a hardware queue for
+// its whole hash. The hub collects the DEVICE_MD5 runs whose decode has been enqueued and
+// hashes up to MD5_MAX_SEGS of them in ONE k_md5_multi launch on its own stream (waiting
+// on each run's decode event), so few launches and few hardware queues carry every chain.
+// A run is flushed into a launch once `runs` are pending, when its batch is waited on, or
+// when its batch polls _ready with its decode done and no hub launch in flight.
+// ---------------------------------------------------------------------------------
+constexpr int MAX_HUB_STREAMS = 4;
+struct Md5Hub {
+    std::mutex mu;
+    hipStream_t st[MAX_HUB_STREAMS] = {};  // launches alternate between the first n_st
+    uint32_t n_st = 1, next = 0;
+    hipEvent_t last = nullptr;  // behind the newest hub launch
+    bool any = false;
+    std::vector<zflac_batch*> pend;
+    uint32_t runs = 6;
+};
+
+DeviceStreams::DeviceStreams() : hub_p(new Md5Hub()), hub(*hub_p) {
+    if (const char* e = std::getenv("ZFLAC_RUN_STREAMS")) n_run = (uint32_t)std::max(1, std::min(atoi(e), MAX_RUN_STREAMS));
+    if (const char* e = std::getenv("ZFLAC_HUB_STREAMS")) hub.n_st = (uint32_t)std::max(1, std::min(atoi(e), MAX_HUB_STREAMS));
+    for (uint32_t i = 0; i < n_run; i++) ck(hipStreamCreateWithFlags(&run[i], hipStreamNonBlocking));
+    for (uint32_t i = 0; i < hub.n_st; i++) ck(hipStreamCreateWithFlags(&hub.st[i], hipStreamNonBlocking));
+    ck(hipEventCreateWithFlags(&hub.last, hipEventDisableTiming));
+    if (const char* e = std::getenv("ZFLAC_MD5_RUNS")) hub.runs = (uint32_t)std::max(1, std::min(atoi(e), MD5_MAX_SEGS));
+}
+
+// (call with the device current)
+DeviceStreams& device_streams(int device) {
+    static std::mutex mu;
+    static std::unordered_map<int, DeviceStreams*> per_device;  // never destroyed: outlives every batch
+    std::lock_guard<std::mutex> lock(mu);
+    DeviceStreams*& d = per_device[device];
+    if (!d) d = new DeviceStreams();
+    return *d;
+}
+
+Md5Hub& md5_hub(int device) { return device_streams(device).hub; }
+
+hipStream_t next_run_stream(int device) {
+    DeviceStreams& d = device_streams(device);
+    std::lock_guard<std::mutex> lock(d.mu);
+    return d.run[d.next++ % d.n_run];
+}
+
+// One launch over every pending run (caller holds hub.mu).
+void hub_flush(Md5Hub& h) {
+    if (h.pend.empty()) return;
+    hipStream_t hs = h.st[h.next++ % h.n_st];
+    Md5Segs sg;
+    std::memset(&sg, 0, sizeof(sg));
+    uint32_t n = 0;
+    for (zflac_batch* b : h.pend) {
+        ck(hipStreamWaitEvent(hs, b->ev_done, 0));
+        sg.jobs[sg.nseg] = b->pipe_jobs.p;
+        sg.dig[sg.nseg] = b->pipe_dig.p;
+        sg.start[sg.nseg] = n;
+        n += (uint32_t)b->pipe_who.size();
+        sg.nseg++;
+    }
+    sg.start[sg.nseg] = n;
+    for (zflac_batch* b : h.pend)  // every run gets the shared launch's time (md5_ms)
+        if (b->flags & ZFLAC_FLAG_TIMING) ck(hipEventRecord(b->ev[8], hs));
+    ck(launch_md5_multi(sg, hs));
+    for (zflac_batch* b : h.pend) {
+        if (b->flags & ZFLAC_FLAG_TIMING) ck(hipEventRecord(b->ev[9], hs));
+        ck(hipMemcpyAsync(b->pipe_pin, b->pipe_dig.p, b->pipe_who.size() * 16, hipMemcpyDeviceToHost, hs));
+        ck(hipEventRecord(b->ev_md5, hs));
+        b->md5_pending = false;
+    }
+    ck(hipEventRecord(h.last, hs));
+    h.any = true;
+    h.pend.clear();
+}
+
+// The run's hash launched (flushing the hub if it is still pending); true if it had to flush.
+void hub_release(zflac_batch* b) {
+    if (!b->md5_pending) return;
+    Md5Hub& h = md5_hub(b->device);
+    std::lock_guard<std::mutex> lock(h.mu);
+    if (b->md5_pending) hub_flush(h);
+}
+
+// Phase 1 of a run: every class's parallel pipeline on the next of the device's run streams,
+// no host wait. Batches submitted back to back overlap on the device (each has its own
+// buffers, consecutive runs different streams): the scan and walk of one run beside the
+// decode of the other.
 void submit_batch(zflac_batch* b) {
     ck(hipSetDevice(b->device));
     const bool timing = (b->flags & ZFLAC_FLAG_TIMING) != 0;
+    // (no wait on the batch's own stream: everything create and finish enqueue there is
+    // synchronized before they return. A marker recorded there would sit in a hardware queue
+    // it may share with a run or md5 hub stream, behind a hash of several milliseconds.)
+    b->rs = next_run_stream(b->device);
     for (size_t ci = 0; ci < b->classes.size(); ci++) {
         Class& C = *b->classes[ci];
         C.redone = false;
         alloc_candidates(C);
         enqueue_class(b, C, timing && ci == 0, timing && ci + 1 == b->classes.size());
     }
-    if (!b->pipe_who.empty()) {  // STREAMINFO MD5 of the streams this run certifies
+    b->md5_hub = !b->pipe_who.empty() && !std::getenv("ZFLAC_MD5_NOHUB");
+    if (!b->pipe_who.empty() && !b->md5_hub) {  // STREAMINFO MD5 of the streams this run certifies
         const uint32_t n = (uint32_t)b->pipe_who.size();
-        if (timing) ck(hipEventRecord(b->ev[8], b->stream));
-        ck(launch_md5(b->pipe_jobs.p, n, b->pipe_dig.p, b->stream));
-        if (timing) ck(hipEventRecord(b->ev[9], b->stream));
-        ck(hipMemcpyAsync(b->pipe_pin, b->pipe_dig.p, (size_t)n * 16, hipMemcpyDeviceToHost, b->stream));
+        if (timing) ck(hipEventRecord(b->ev[8], b->rs));
+        ck(launch_md5(b->pipe_jobs.p, n, b->pipe_dig.p, b->rs));
+        if (timing) ck(hipEventRecord(b->ev[9], b->rs));
+        ck(hipMemcpyAsync(b->pipe_pin, b->pipe_dig.p, (size_t)n * 16, hipMemcpyDeviceToHost, b->rs));
     }
-    ck(hipEventRecord(b->ev_done, b->stream));  // zflac_hip_batch_ready
+    ck(hipEventRecord(b->ev_done, b->rs));  // zflac_hip_batch_ready
+    if (b->md5_hub) {  // the hash of the streams this run certifies, in the device's md5 hub
+        Md5Hub& h = md5_hub(b->device);
+        std::lock_guard<std::mutex> lock(h.mu);
+        b->md5_pending = true;
+        h.pend.push_back(b);
+        if (h.pend.size() >= std::min<uint32_t>(h.runs, MD5_MAX_SEGS)) hub_flush(h);
+    }
 }
 
 // Phase 2: wait for the pipeline, redo a class whose candidate table overflowed (grown,
@@ -1027,7 +1167,12 @@ void submit_batch(zflac_batch* b) {
 void finish_batch(zflac_batch* b) {
     ck(hipSetDevice(b->device));
     const bool timing = (b->flags & ZFLAC_FLAG_TIMING) != 0;
-    ck(hipStreamSynchronize(b->stream));
+    ck(hipEventSynchronize(b->ev_done));  // the run, on its run stream
+    b->rs = b->stream;  // from here on (regrowth, rest launch, planner): the batch's own stream
+    if (b->md5_hub) {  // the run's hash (and its digests' read-back) in the md5 hub
+        hub_release(b);
+        ck(hipEventSynchronize(b->ev_md5));
+    }
     uint32_t rest_launches = 0;
     for (size_t ci = 0; ci < b->classes.size(); ci++) {
         Class& C = *b->classes[ci];
@@ -1402,7 +1547,9 @@ int create_batch(const zflac_stream* streams, size_t n, int device, int flags, z
     b->flags = flags;
     try {
         ck(hipSetDevice(device));
+        (void)device_streams(device);  // the run and md5 hub streams first (their own hardware queues)
         ck(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+        b->rs = b->stream;
         if (const char* fp = std::getenv("ZFLAC_FRONT_PRIORITY"); fp && fp[0] == '1') {
             int least = 0, greatest = 0;
             ck(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -1413,6 +1560,7 @@ int create_batch(const zflac_stream* streams, size_t n, int device, int flags, z
         // record, which would otherwise slow the kernel after it
         for (auto& e : b->ev) ck(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         ck(hipEventCreateWithFlags(&b->ev_done, hipEventDisableTiming));
+        ck(hipEventCreateWithFlags(&b->ev_md5, hipEventDisableTiming));
         const double t0 = now_ms();
         b->streams.resize(n);
         for (size_t i = 0; i < n; i++) {
@@ -1460,6 +1608,8 @@ int create_batch(const zflac_stream* streams, size_t n, int device, int flags, z
 }
 
 }  // namespace
+
+void hub_release_ext(zflac_batch* b) { hub_release(b); }
 }  // namespace zflac
 
 // ---------------------------------------------------------------------------------
@@ -1514,7 +1664,9 @@ int zflac_hip_batch_create(const zflac_stream* streams, size_t n, int device, in
 // reallocates.
 static void drain_failed_submit(zflac_batch* b) {
     (void)hipStreamSynchronize(b->stream);
+    if (b->rs) (void)hipStreamSynchronize(b->rs);
     if (b->front) (void)hipStreamSynchronize(b->front);
+    b->rs = b->stream;
     b->submitted = false;
 }
 
@@ -1557,7 +1709,20 @@ int zflac_hip_batch_wait(zflac_batch* b) {
 
 int zflac_hip_batch_ready(zflac_batch* b) {
     if (!b || !b->submitted) return -E_INVALID_ARGUMENT;
-    const hipError_t e = hipEventQuery(b->ev_done);
+    hipError_t e = hipEventQuery(b->ev_done);
+    if (e == hipSuccess && b->md5_hub) {
+        if (b->md5_pending) {  // decoded, hash not launched: launch it if the hub is idle
+            try {
+                Md5Hub& h = md5_hub(b->device);
+                std::lock_guard<std::mutex> lock(h.mu);
+                if (b->md5_pending && (!h.any || hipEventQuery(h.last) == hipSuccess)) hub_flush(h);
+            } catch (const DeviceError&) {
+                return -E_DEVICE;
+            }
+            return 0;
+        }
+        e = hipEventQuery(b->ev_md5);
+    }
     if (e == hipSuccess) return 1;
     if (e == hipErrorNotReady) return 0;
     return -E_DEVICE;

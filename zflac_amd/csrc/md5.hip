@@ -190,20 +190,17 @@ __device__ __forceinline__ uint64_t hash_units_any(const Md5Job& j, uint32_t st[
                                                           : hash_units<MODE, false>(j, st);
 }
 
-__global__ __launch_bounds__(64) void k_md5(const Md5Job* __restrict__ jobs, uint32_t n_jobs,
-                                            uint32_t* __restrict__ digests) {
-    const uint32_t t = blockIdx.x * 64 + threadIdx.x;
-    if (t >= n_jobs) return;
+// One stream's digest into out[0..3].
+__device__ __forceinline__ void md5_job(const Md5Job& j, uint32_t* __restrict__ out) {
 #ifdef ZFLAC_MD5_PRIO
     // (experiment) the hash waves ahead of the decode waves they share SIMDs with: the
     // serial chains then run at the pace of a wave alone, but the decode waves slow down
     __builtin_amdgcn_s_setprio(ZFLAC_MD5_PRIO);
 #endif
-    const Md5Job j = jobs[t];
     uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
     if (j.status && *j.status) {  // not certified by this run: the host hashes it after the planner
 #pragma unroll
-        for (int i = 0; i < 4; i++) digests[(uint64_t)t * 4 + i] = 0u;
+        for (int i = 0; i < 4; i++) out[i] = 0u;
         return;
     }
     const uint64_t L = j.n * (uint64_t)j.width;  // message bytes
@@ -236,7 +233,25 @@ __global__ __launch_bounds__(64) void k_md5(const Md5Job* __restrict__ jobs, uin
         compress(st, m);
     }
 #pragma unroll
-    for (int i = 0; i < 4; i++) digests[(uint64_t)t * 4 + i] = st[i];
+    for (int i = 0; i < 4; i++) out[i] = st[i];
+}
+
+__global__ __launch_bounds__(64) void k_md5(const Md5Job* __restrict__ jobs, uint32_t n_jobs,
+                                            uint32_t* __restrict__ digests) {
+    const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+    if (t >= n_jobs) return;
+    md5_job(jobs[t], digests + (uint64_t)t * 4);
+}
+
+// The jobs of several runs (one segment each: several batches' runs hashed by one launch,
+// md5 hub in host.cpp): lane t hashes job t - start[s] of the segment s holding t.
+__global__ __launch_bounds__(64) void k_md5_multi(Md5Segs sg) {
+    const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+    if (t >= sg.start[sg.nseg]) return;
+    uint32_t s = 0;
+    while (s + 1 < sg.nseg && sg.start[s + 1] <= t) s++;
+    const uint32_t k = t - sg.start[s];
+    md5_job(sg.jobs[s][k], sg.dig[s] + (uint64_t)k * 4);
 }
 
 }  // namespace
@@ -244,6 +259,13 @@ __global__ __launch_bounds__(64) void k_md5(const Md5Job* __restrict__ jobs, uin
 hipError_t launch_md5(const Md5Job* jobs, uint32_t n_jobs, uint32_t* digests, hipStream_t st) {
     if (!n_jobs) return hipSuccess;
     hipLaunchKernelGGL(k_md5, dim3((n_jobs + 63) / 64), dim3(64), 0, st, jobs, n_jobs, digests);
+    return hipGetLastError();
+}
+
+hipError_t launch_md5_multi(const Md5Segs& sg, hipStream_t st) {
+    const uint32_t n = sg.start[sg.nseg];
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_md5_multi, dim3((n + 63) / 64), dim3(64), 0, st, sg);
     return hipGetLastError();
 }
 
