@@ -145,6 +145,41 @@ def test_device_md5_every_class(gpu_ready):
     b.close()
 
 
+@pytest.mark.parametrize("loads", ["coop", "lane"])
+@pytest.mark.parametrize("name", ["mono8_lpc3", "c3_ms16_lpc8", "stereo12_ms", "ms20_lpc16_escape",
+                                  "c4_24bit_lpc32_wasted", "stereo32", "stereo31_ls_loud"])
+def test_device_md5_cooperative_loads(gpu_ready, name, loads):
+    """One class per batch (every job in one mode: k_md5_coop, the wave's 64 streams read
+    through LDS; ZFLAC_MD5_LANE_LOADS=1 forces k_md5). 70 streams (a second, partial wave
+    whose idle lanes only help load) of ragged lengths (lanes leave the unit loop at
+    different units); one stream's MD5 corrupted. Digests equal STREAMINFO and hashlib."""
+    cfg = PARITY_CONFIGS[name]
+    bs = cfg["block_size"]
+    datas = [synth.generate(**dict(cfg, seed=4000 + i, n_samples=bs * (1 + (i * 7) % 5) + (i * 13) % 97)).flac
+             for i in range(70)]
+    bad = bytearray(datas[65])
+    bad[30] ^= 0x01  # a STREAMINFO MD5 byte
+    datas[65] = bytes(bad)
+    if loads == "lane":
+        os.environ["ZFLAC_MD5_LANE_LOADS"] = "1"
+    try:
+        b = zflac_amd.Batch(datas, device_md5=True, timing=True)
+    finally:
+        os.environ.pop("ZFLAC_MD5_LANE_LOADS", None)
+    for _ in range(2):  # the second run reuses the batch (and the md5 hub)
+        b.run()
+        for i, data in enumerate(datas):
+            rc, _ = b.info(i)
+            if i == 65:
+                assert errors.NAMES.get(rc) == "InvalidChecksum", rc
+                continue
+            assert rc == 0, (i, rc)
+            assert b.md5(i) == _streaminfo_md5(data), i
+    r = oracle.decode(datas[3])
+    assert b.md5(3) == _md5_pre_justify(r.samples, r.bits_per_sample)
+    b.close()
+
+
 def test_device_md5_c5_shard(gpu_ready):
     """C5-shaped members (32 frames, 131072 samples/ch), device MD5 against STREAMINFO."""
     streams = synth.generate_many([synth.config_c5(i) for i in range(130)])

@@ -99,8 +99,10 @@ static hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_fram
 hipError_t launch_verify(const VerifyArgs& a, uint32_t max_items, hipStream_t st);
 hipError_t launch_crc16(const Crc16Args& a, uint32_t max_frames, hipStream_t st);
 hipError_t launch_sync_list(const SyncListArgs& a, hipStream_t st);
-hipError_t launch_md5(const Md5Job* jobs, uint32_t n_jobs, uint32_t* digests, hipStream_t st);
-hipError_t launch_md5_multi(const Md5Segs& sg, hipStream_t st);
+// coop_mode: the Md5Mode every job shares with 16-byte aligned samples (the cooperative-load
+// kernel), or -1 (lane-per-stream loads)
+hipError_t launch_md5(const Md5Job* jobs, uint32_t n_jobs, uint32_t* digests, hipStream_t st, int coop_mode);
+hipError_t launch_md5_multi(const Md5Segs& sg, hipStream_t st, int coop_mode);
 
 namespace {
 
@@ -377,6 +379,7 @@ struct zflac_batch {
     // the run's k_verify (pipe_who[k] = stream of job k, longest first); its digests land in
     // pinned memory with the run's other read-backs
     zflac::DevBuf<zflac::Md5Job> pipe_jobs;
+    int pipe_coop = -1;  // coop_mode_of(the pipe jobs)
     zflac::DevBuf<uint32_t> pipe_dig;
     std::vector<uint32_t> pipe_who;
     uint32_t* pipe_pin = nullptr;
@@ -1095,7 +1098,9 @@ void hub_flush(Md5Hub& h) {
     Md5Segs sg;
     std::memset(&sg, 0, sizeof(sg));
     uint32_t n = 0;
+    int coop = h.pend[0]->pipe_coop;  // the cooperative kernel only when every run's jobs allow it
     for (zflac_batch* b : h.pend) {
+        if (b->pipe_coop != coop) coop = -1;
         ck(hipStreamWaitEvent(hs, b->ev_done, 0));
         sg.jobs[sg.nseg] = b->pipe_jobs.p;
         sg.dig[sg.nseg] = b->pipe_dig.p;
@@ -1106,7 +1111,7 @@ void hub_flush(Md5Hub& h) {
     sg.start[sg.nseg] = n;
     for (zflac_batch* b : h.pend)  // every run gets the shared launch's time (md5_ms)
         if (b->flags & ZFLAC_FLAG_TIMING) ck(hipEventRecord(b->ev[8], hs));
-    ck(launch_md5_multi(sg, hs));
+    ck(launch_md5_multi(sg, hs, coop));
     for (zflac_batch* b : h.pend) {
         if (b->flags & ZFLAC_FLAG_TIMING) ck(hipEventRecord(b->ev[9], hs));
         ck(hipMemcpyAsync(b->pipe_pin, b->pipe_dig.p, b->pipe_who.size() * 16, hipMemcpyDeviceToHost, hs));
@@ -1147,7 +1152,7 @@ void submit_batch(zflac_batch* b) {
     if (!b->pipe_who.empty() && !b->md5_hub) {  // STREAMINFO MD5 of the streams this run certifies
         const uint32_t n = (uint32_t)b->pipe_who.size();
         if (timing) ck(hipEventRecord(b->ev[8], b->rs));
-        ck(launch_md5(b->pipe_jobs.p, n, b->pipe_dig.p, b->rs));
+        ck(launch_md5(b->pipe_jobs.p, n, b->pipe_dig.p, b->rs, b->pipe_coop));
         if (timing) ck(hipEventRecord(b->ev[9], b->rs));
         ck(hipMemcpyAsync(b->pipe_pin, b->pipe_dig.p, (size_t)n * 16, hipMemcpyDeviceToHost, b->rs));
     }
@@ -1428,6 +1433,15 @@ Md5Job md5_job(const StreamState& s, const void* data, uint64_t n, const uint32_
     return j;
 }
 
+// The Md5Mode all `jobs` share when every one's samples are 16-byte aligned: k_md5_coop
+// (cooperative loads) can hash them; else -1 (k_md5, each lane its own loads).
+int coop_mode_of(const std::vector<Md5Job>& jobs) {
+    if (jobs.empty() || std::getenv("ZFLAC_MD5_LANE_LOADS")) return -1;
+    for (const Md5Job& j : jobs)
+        if (j.mode != jobs[0].mode || (reinterpret_cast<uintptr_t>(j.data) & 15) != 0) return -1;
+    return (int)jobs[0].mode;
+}
+
 // Order of `jobs` longest message first: the lanes of a wave then run chains of similar length.
 std::vector<uint32_t> longest_first(const std::vector<Md5Job>& jobs) {
     std::vector<uint32_t> ord(jobs.size());
@@ -1472,6 +1486,7 @@ void plan_md5_pipeline(zflac_batch* b) {
         sorted[k] = jobs[ord[k]];
         b->pipe_who[k] = who[ord[k]];
     }
+    b->pipe_coop = coop_mode_of(sorted);
     b->pipe_jobs.alloc(sorted.size());
     b->pipe_dig.alloc(sorted.size() * 4);
     ck(hipMemcpy(b->pipe_jobs.p, sorted.data(), sorted.size() * sizeof(Md5Job), hipMemcpyHostToDevice));
@@ -1496,7 +1511,7 @@ void run_md5_device(zflac_batch* b, const std::vector<uint32_t>& which, bool tim
     ck(hipMemcpyAsync(b->md5_jobs.p, sorted.data(), sorted.size() * sizeof(Md5Job), hipMemcpyHostToDevice,
                       b->stream));
     if (timing) ck(hipEventRecord(b->ev[5], b->stream));
-    ck(launch_md5(b->md5_jobs.p, (uint32_t)sorted.size(), b->md5_dig.p, b->stream));
+    ck(launch_md5(b->md5_jobs.p, (uint32_t)sorted.size(), b->md5_dig.p, b->stream, coop_mode_of(sorted)));
     if (timing) ck(hipEventRecord(b->ev[6], b->stream));
     std::vector<uint32_t> dig(sorted.size() * 4);
     ck(hipMemcpyAsync(dig.data(), b->md5_dig.p, dig.size() * 4, hipMemcpyDeviceToHost, b->stream));

@@ -12,10 +12,11 @@
 // of the compression that uses them), 64 dependent rounds of ~5 VALU ops (gfx950's
 // v_bitop3_b32 makes each round function one instruction).
 //
-// A lane's time is its stream's chain (~4 cycles per VALU op for one wave alone), so a
-// batch's hash takes about as long as its longest stream, whatever the stream count; the
-// batch API enqueues it behind the decode of the same run (zflac_hip_batch_submit), so the
-// runs of other batches in flight fill the SIMDs meanwhile.
+// A lane's time is its stream's chain (~4 dependent VALU ops per round), so a batch's hash
+// takes about as long as its longest stream, whatever the stream count. Runs are hashed by
+// the device's md5 hub (host.cpp): one k_md5_multi launch over the certified streams of
+// several runs, on a stream of its own, while the runs of other batches decode. A wave
+// reads its 64 streams' data cooperatively through LDS (hash_units_coop).
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -154,11 +155,19 @@ __device__ __forceinline__ uint64_t hash_units(const Md5Job& j, uint32_t st[4]) 
     const uint32_t* p = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(j.data) & ~(uintptr_t)3);
     uint32_t ba[UNIT_WORDS + 1], bb[UNIT_WORDS + 1];
     auto load = [&](uint64_t u, uint32_t* r) {
+#if defined(ZFLAC_MD5_NOLOAD)  // (diagnostic) no memory reads: the chain alone; wrong digests
+#pragma unroll
+        for (int i = 0; i <= UNIT_WORDS; i++) r[i] = (uint32_t)u * 0x9e3779b9u + i;
+        return;
+#elif defined(ZFLAC_MD5_L2HIT)  // (diagnostic) every unit re-reads the stream's first 1 KiB; wrong digests
+        u &= 3;
+#endif
         const uint32_t* q = p + u * UNIT_WORDS;
         if constexpr (VEC) {
 #pragma unroll
             for (int i = 0; i < UNIT_WORDS / 4; i++) {
-                const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q) + i);
+                const u32x4 v = __builtin_nontemporal_load(
+                    reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(reinterpret_cast<uintptr_t>(q)) + i);
                 r[4 * i] = v[0];
                 r[4 * i + 1] = v[1];
                 r[4 * i + 2] = v[2];
@@ -190,28 +199,83 @@ __device__ __forceinline__ uint64_t hash_units_any(const Md5Job& j, uint32_t st[
                                                           : hash_units<MODE, false>(j, st);
 }
 
-// One stream's digest into out[0..3].
-__device__ __forceinline__ void md5_job(const Md5Job& j, uint32_t* __restrict__ out) {
-#ifdef ZFLAC_MD5_PRIO
-    // (experiment) the hash waves ahead of the decode waves they share SIMDs with: the
-    // serial chains then run at the pace of a wave alone, but the decode waves slow down
-    __builtin_amdgcn_s_setprio(ZFLAC_MD5_PRIO);
-#endif
-    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
-    if (j.status && *j.status) {  // not certified by this run: the host hashes it after the planner
+// Wave-cooperative unit loop: every lane of the wave calls it (lanes with `act` false only
+// help load). Lane-per-stream loads touch 64 streams' cache lines per wave-instruction; here
+// wave-instruction i instead reads the 256-byte units of streams 4i..4i+3 (four 256-byte
+// runs: the lane-per-stream form's 64 lines become 8), the wave's 64 units go through one
+// 16 KiB LDS tile, and each lane then reads its own stream's unit from it. Row s of the tile
+// is stream s (lane s); its piece pc (16 bytes) sits at slot (pc + s) & 15, so the 64 lanes'
+// reads of one piece fall on different banks (a plain 256-byte row stride puts them on one).
+// The next unit's loads are in flight in registers while the current one is compressed.
+// Needs every active lane's samples 16-byte aligned (certified streams: see hash_units) and
+// one MODE across the wave. Returns message bytes hashed.
+template <int MODE>
+__device__ __forceinline__ uint64_t hash_units_coop(const Md5Job& j, bool act, uint32_t st[4], u32x4* tile) {
+    constexpr uint64_t MSG_PER_UNIT = MODE == MD5_S24 ? 192 : 256;
+    const uint32_t L = threadIdx.x & 63u;
+    const uint32_t nu = act ? (uint32_t)min(j.n * (uint64_t)j.width / MSG_PER_UNIT, (uint64_t)0xFFFFFFFFu) : 0u;
+    const uint64_t base = reinterpret_cast<uintptr_t>(j.data);
+    uint64_t src[16];  // this lane's 16 bytes of stream 4i + L/16's unit 0 (piece (L - s) & 15)
+    uint32_t nus[16];
 #pragma unroll
-        for (int i = 0; i < 4; i++) out[i] = 0u;
-        return;
+    for (int i = 0; i < 16; i++) {
+        const int sl = 4 * i + (int)(L >> 4);
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)base, sl), hi = (uint32_t)__shfl((int)(uint32_t)(base >> 32), sl);
+        src[i] = (((uint64_t)hi << 32) | lo) + ((L - (uint32_t)sl) & 15u) * 16u;
+        nus[i] = (uint32_t)__shfl((int)nu, sl);
     }
+    uint32_t maxu = nu;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) maxu = max(maxu, (uint32_t)__shfl_xor((int)maxu, o));
+    u32x4 R[16];
+    auto load = [&](uint32_t u) {
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            if (u < nus[i])  // global (not flat) loads: a flat load would also hold lgkmcnt, i.e. the tile reads
+                R[i] = __builtin_nontemporal_load(
+                    reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(src[i] + (uint64_t)u * 256u));
+    };
+    if (maxu) load(0);
+    const u32x4* row = tile + L * 16u;
+    for (uint32_t u = 0; u < maxu; u++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) tile[i * 64 + L] = R[i];  // row 4i + L/16, slot L & 15
+        __syncthreads();
+        if (u + 1 < maxu) load(u + 1);
+        if (u < nu) {
+            if constexpr (MODE == MD5_S24) {
+                uint32_t cur[UNIT_WORDS + 1];
+#pragma unroll
+                for (int pc = 0; pc < 16; pc++) {
+                    const u32x4 v = row[(pc + L) & 15u];
+#pragma unroll
+                    for (int e = 0; e < 4; e++) cur[4 * pc + e] = v[e];
+                }
+                cur[UNIT_WORDS] = 0u;
+                hash_unit<MODE>(cur, 0u, j.js, st);
+            } else {
+#pragma unroll
+                for (int blk = 0; blk < 4; blk++) {
+                    uint32_t m[16];
+#pragma unroll
+                    for (int pc = 0; pc < 4; pc++) {
+                        const u32x4 v = row[(blk * 4 + pc + L) & 15u];
+#pragma unroll
+                        for (int e = 0; e < 4; e++) m[4 * pc + e] = unjustify_word<MODE>(v[e], j.js);
+                    }
+                    compress(st, m);
+                }
+            }
+        }
+        __syncthreads();  // every lane's reads of the tile before the next unit's writes
+    }
+    return (uint64_t)nu * MSG_PER_UNIT;
+}
+
+// The tail blocks of one stream (the message bytes after `done`, 0x80, zero fill, the
+// 64-bit little-endian bit length) and its digest into out[0..3].
+__device__ __forceinline__ void md5_tail(const Md5Job& j, uint64_t done, uint32_t st[4], uint32_t* __restrict__ out) {
     const uint64_t L = j.n * (uint64_t)j.width;  // message bytes
-    uint64_t done;                                // message bytes hashed by the unit loop
-    switch (j.mode) {
-        case MD5_RAW: done = hash_units_any<MD5_RAW>(j, st); break;
-        case MD5_S16_SHIFT: done = hash_units_any<MD5_S16_SHIFT>(j, st); break;
-        case MD5_S32_SHIFT: done = hash_units_any<MD5_S32_SHIFT>(j, st); break;
-        default: done = hash_units_any<MD5_S24>(j, st); break;
-    }
-    // tail: remaining message bytes, 0x80, zero fill, 64-bit little-endian bit length
     uint32_t m[16];
     const uint64_t r = L - done;
     const uint32_t tb = (uint32_t)((r + 8) / 64 + 1);
@@ -236,6 +300,44 @@ __device__ __forceinline__ void md5_job(const Md5Job& j, uint32_t* __restrict__ 
     for (int i = 0; i < 4; i++) out[i] = st[i];
 }
 
+__device__ __forceinline__ void md5_prio() {
+#ifdef ZFLAC_MD5_PRIO
+    // (experiment) the hash waves ahead of the decode waves they share SIMDs with: the
+    // serial chains then run at the pace of a wave alone, but the decode waves slow down
+    __builtin_amdgcn_s_setprio(ZFLAC_MD5_PRIO);
+#endif
+}
+
+// One stream's digest into out[0..3], the lane's own loads (any mode and alignment).
+__device__ __forceinline__ void md5_job(const Md5Job& j, uint32_t* __restrict__ out) {
+    md5_prio();
+    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    if (j.status && *j.status) {  // not certified by this run: the host hashes it after the planner
+#pragma unroll
+        for (int i = 0; i < 4; i++) out[i] = 0u;
+        return;
+    }
+    uint64_t done;  // message bytes hashed by the unit loop
+    switch (j.mode) {
+        case MD5_RAW: done = hash_units_any<MD5_RAW>(j, st); break;
+        case MD5_S16_SHIFT: done = hash_units_any<MD5_S16_SHIFT>(j, st); break;
+        case MD5_S32_SHIFT: done = hash_units_any<MD5_S32_SHIFT>(j, st); break;
+        default: done = hash_units_any<MD5_S24>(j, st); break;
+    }
+    md5_tail(j, done, st, out);
+}
+
+// The jobs of several runs (one segment each: several batches' runs hashed by one launch,
+// md5 hub in host.cpp): lane t's job is job t - start[s] of the segment s holding t.
+__device__ __forceinline__ const Md5Job* seg_job(const Md5Segs& sg, uint32_t t, uint32_t*& out) {
+    if (t >= sg.start[sg.nseg]) return nullptr;
+    uint32_t s = 0;
+    while (s + 1 < sg.nseg && sg.start[s + 1] <= t) s++;
+    const uint32_t k = t - sg.start[s];
+    out = sg.dig[s] + (uint64_t)k * 4;
+    return sg.jobs[s] + k;
+}
+
 __global__ __launch_bounds__(64) void k_md5(const Md5Job* __restrict__ jobs, uint32_t n_jobs,
                                             uint32_t* __restrict__ digests) {
     const uint32_t t = blockIdx.x * 64 + threadIdx.x;
@@ -243,29 +345,62 @@ __global__ __launch_bounds__(64) void k_md5(const Md5Job* __restrict__ jobs, uin
     md5_job(jobs[t], digests + (uint64_t)t * 4);
 }
 
-// The jobs of several runs (one segment each: several batches' runs hashed by one launch,
-// md5 hub in host.cpp): lane t hashes job t - start[s] of the segment s holding t.
 __global__ __launch_bounds__(64) void k_md5_multi(Md5Segs sg) {
-    const uint32_t t = blockIdx.x * 64 + threadIdx.x;
-    if (t >= sg.start[sg.nseg]) return;
-    uint32_t s = 0;
-    while (s + 1 < sg.nseg && sg.start[s + 1] <= t) s++;
-    const uint32_t k = t - sg.start[s];
-    md5_job(sg.jobs[s][k], sg.dig[s] + (uint64_t)k * 4);
+    uint32_t* out = nullptr;
+    const Md5Job* j = seg_job(sg, blockIdx.x * 64 + threadIdx.x, out);
+    if (j) md5_job(*j, out);
+}
+
+// Every job of the launch in mode MODE with 16-byte aligned samples (the host checks):
+// the wave's lanes load cooperatively (hash_units_coop); lanes past the job list, or whose
+// stream this run did not certify, only help load.
+template <int MODE>
+__global__ __launch_bounds__(64) void k_md5_coop(Md5Segs sg) {
+    __shared__ u32x4 tile[64 * 16];
+    md5_prio();
+    uint32_t* out = nullptr;
+    const Md5Job* jp = seg_job(sg, blockIdx.x * 64 + threadIdx.x, out);
+    Md5Job j{};
+    if (jp) j = *jp;
+    const bool act = jp && !(j.status && *j.status);
+    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    const uint64_t done = hash_units_coop<MODE>(j, act, st, tile);
+    if (act) {
+        md5_tail(j, done, st, out);
+    } else if (jp) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) out[i] = 0u;
+    }
 }
 
 }  // namespace
 
-hipError_t launch_md5(const Md5Job* jobs, uint32_t n_jobs, uint32_t* digests, hipStream_t st) {
-    if (!n_jobs) return hipSuccess;
-    hipLaunchKernelGGL(k_md5, dim3((n_jobs + 63) / 64), dim3(64), 0, st, jobs, n_jobs, digests);
+hipError_t launch_md5_multi(const Md5Segs& sg, hipStream_t st, int coop_mode) {
+    const uint32_t n = sg.start[sg.nseg];
+    if (!n) return hipSuccess;
+    const dim3 g((n + 63) / 64), b(64);
+    switch (coop_mode) {
+        case MD5_RAW: hipLaunchKernelGGL(k_md5_coop<MD5_RAW>, g, b, 0, st, sg); break;
+        case MD5_S16_SHIFT: hipLaunchKernelGGL(k_md5_coop<MD5_S16_SHIFT>, g, b, 0, st, sg); break;
+        case MD5_S32_SHIFT: hipLaunchKernelGGL(k_md5_coop<MD5_S32_SHIFT>, g, b, 0, st, sg); break;
+        case MD5_S24: hipLaunchKernelGGL(k_md5_coop<MD5_S24>, g, b, 0, st, sg); break;
+        default: hipLaunchKernelGGL(k_md5_multi, g, b, 0, st, sg); break;
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_md5_multi(const Md5Segs& sg, hipStream_t st) {
-    const uint32_t n = sg.start[sg.nseg];
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_md5_multi, dim3((n + 63) / 64), dim3(64), 0, st, sg);
+hipError_t launch_md5(const Md5Job* jobs, uint32_t n_jobs, uint32_t* digests, hipStream_t st, int coop_mode) {
+    if (!n_jobs) return hipSuccess;
+    if (coop_mode >= 0) {
+        Md5Segs sg;
+        sg.jobs[0] = jobs;
+        sg.dig[0] = digests;
+        sg.start[0] = 0;
+        sg.start[1] = n_jobs;
+        sg.nseg = 1;
+        return launch_md5_multi(sg, st, coop_mode);
+    }
+    hipLaunchKernelGGL(k_md5, dim3((n_jobs + 63) / 64), dim3(64), 0, st, jobs, n_jobs, digests);
     return hipGetLastError();
 }
 
