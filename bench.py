@@ -98,9 +98,16 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-md5", action="store_true", help="skip the device-MD5 leg")
-    ap.add_argument("--md5-inflight", type=int, default=12, help="batches in flight in the decode+MD5 leg")
-    ap.add_argument("--md5-hw-queues", type=int, default=16,
-                    help="GPU_MAX_HW_QUEUES of the decode+MD5 leg's process (one HIP stream per batch in flight)")
+    ap.add_argument("--md5-inflight", type=int, default=24, help="batches in flight in the decode+MD5 leg")
+    ap.add_argument("--md5-steps", type=int, default=96,
+                    help="timed runs of the decode+MD5 leg (its last hashes, ~8 ms each, end the timed region)")
+    ap.add_argument("--md5-run-streams", type=int, default=5,
+                    help="decode+MD5 leg: the library's run streams (ZFLAC_RUN_STREAMS)")
+    ap.add_argument("--md5-hub-streams", type=int, default=2,
+                    help="decode+MD5 leg: md5 hub streams (ZFLAC_HUB_STREAMS), each launch hashing --md5-runs runs")
+    ap.add_argument("--md5-runs", type=int, default=6, help="decode+MD5 leg: runs per md5 hub launch (ZFLAC_MD5_RUNS)")
+    ap.add_argument("--md5-hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES of the decode+MD5 leg's process (default: run + hub streams)")
     ap.add_argument("--sched", choices=["rr", "ready"], default="rr",
                     help="headline runs in flight: round robin, or whichever batch finished first")
     ap.add_argument("--md5-leg-child", action="store_true", help=argparse.SUPPRESS)
@@ -327,12 +334,17 @@ def run_ready_order(batches, k: int, on_done=None) -> None:
 
 def md5_leg(args, streams, device: int, barrier=lambda: None):
     """decode + STREAMINFO MD5 of every stream of the shard: batches created with
-    ZFLAC_FLAG_DEVICE_MD5, whose k_md5 zflac_hip_batch_submit enqueues right behind each
-    run's kernels; `md5_inflight` batches in completion order (run_ready_order), so one batch's hash (a serial chain
-    per stream, ~7 ms for this shard) runs beside the other batches' runs."""
+    ZFLAC_FLAG_DEVICE_MD5; each run's certified streams go to the device's md5 hub, which
+    hashes several runs per k_md5_coop launch on streams of its own (a serial chain per
+    stream, ~7-9 ms for this shard) while other batches' runs decode on the run streams.
+    `md5_inflight` batches in completion order (run_ready_order), `md5_steps` timed runs."""
+    for k, v in (("ZFLAC_RUN_STREAMS", args.md5_run_streams), ("ZFLAC_HUB_STREAMS", args.md5_hub_streams),
+                 ("ZFLAC_MD5_RUNS", args.md5_runs)):
+        os.environ.setdefault(k, str(v))  # read by the library when it creates the device's streams
     import zflac_amd
 
-    k_md5 = max(1, min(args.md5_inflight, args.steps))
+    n_steps = args.md5_steps
+    k_md5 = max(1, min(args.md5_inflight, n_steps))
     mbs = [zflac_amd.Batch(streams, device=device, timing=True, device_md5=True) for _ in range(k_md5)]
     rec = []
 
@@ -343,7 +355,7 @@ def md5_leg(args, streams, device: int, barrier=lambda: None):
     rec.clear()
     barrier()
     t1 = time.perf_counter()
-    steps(args.steps)
+    steps(n_steps)
     barrier()
     el = time.perf_counter() - t1
     samples = mbs[0].timings().samples
@@ -351,14 +363,15 @@ def md5_leg(args, streams, device: int, barrier=lambda: None):
     ok = all(mb.info(i)[0] == 0 and mb.md5(i) == s[26:42] for mb in mbs for i, s in enumerate(streams))
     for mb in mbs:
         mb.close()
-    return {"kernel": "k_md5", "md5_ms": round(float(np.mean(rec)), 4), "all_match": ok, "inflight": k_md5,
-            "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-            "decode_plus_md5_msps_rank0": round(samples * args.steps / el / 1e6, 1),
-            "ms_per_step": round(el / args.steps * 1e3, 4),
-            "md5_waves_per_simd": round(k_md5 * -(-len(streams) // 64) / 1024, 3),
+    return {"kernel": "k_md5_coop", "md5_ms": round(float(np.mean(rec)), 4), "all_match": ok, "inflight": k_md5,
+            "steps": n_steps, "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+            "run_streams": os.environ.get("ZFLAC_RUN_STREAMS"), "hub_streams": os.environ.get("ZFLAC_HUB_STREAMS"),
+            "runs_per_hub_launch": os.environ.get("ZFLAC_MD5_RUNS"),
+            "decode_plus_md5_msps_rank0": round(samples * n_steps / el / 1e6, 1),
+            "ms_per_step": round(el / n_steps * 1e3, 4),
             "hashed_bytes_rank0": int(out_bytes),
-            "note": "decode + STREAMINFO MD5 of every stream, k_md5 (one lane per stream) enqueued behind each "
-                    "run; md5_ms = k_md5 launch time while overlapped; not in `value`"}
+            "note": "decode + STREAMINFO MD5 of every stream (one lane per stream, the wave's loads through LDS); "
+                    "md5_ms = one md5 hub launch (several runs) while overlapped; not in `value`"}
 
 
 def start_md5_child(args):
@@ -368,12 +381,15 @@ def start_md5_child(args):
     anything: it blocks on its stdin until md5_leg_in_child sends it this rank's shard. Per
     rank that is two processes (this one and the child) and host_threads(world) host threads."""
     cmd = [sys.executable, os.path.abspath(__file__), "--md5-leg-child", "--steps", str(args.steps), "--warmup",
-           str(args.warmup), "--streams-per-gpu", str(args.streams_per_gpu), "--md5-inflight", str(args.md5_inflight)]
+           str(args.warmup), "--streams-per-gpu", str(args.streams_per_gpu), "--md5-inflight", str(args.md5_inflight),
+           "--md5-steps", str(args.md5_steps), "--md5-run-streams", str(args.md5_run_streams),
+           "--md5-hub-streams", str(args.md5_hub_streams), "--md5-runs", str(args.md5_runs)]
     if args.same_device:
         cmd.append("--same-device")
     if args.dry_run:
         cmd.append("--dry-run")
-    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(args.md5_hw_queues))
+    q = args.md5_hw_queues or args.md5_run_streams + args.md5_hub_streams  # one hardware queue per stream
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(q))
     return subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE)
 
 

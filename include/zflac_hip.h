@@ -124,7 +124,9 @@ int zflac_hip_batch_create(const zflac_stream *streams, size_t n, int device, in
  * zflac errors are reported by zflac_hip_batch_info. */
 int zflac_hip_batch_run(zflac_batch *b);
 /* zflac_hip_batch_run in two halves, so that runs of different batches overlap on the
- * device: _submit enqueues the run's kernels on the batch's own HIP stream and returns;
+ * device: _submit enqueues the run's kernels on the next of the device's run streams
+ * (ZFLAC_RUN_STREAMS, default 3) and returns; with ZFLAC_FLAG_DEVICE_MD5 the run's hash
+ * goes to the device's md5 hub (one launch over several runs, streams of its own);
  * _wait blocks until they finish and produces the per-stream results (the sequential
  * planner, CRC-16 and MD5 legs run here). A batch has at most one run in flight: _submit
  * on a submitted batch and _wait without one return ZFLAC_E_INVALID_ARGUMENT, and results
@@ -134,7 +136,9 @@ int zflac_hip_batch_submit(zflac_batch *b);
 int zflac_hip_batch_wait(zflac_batch *b);
 /* (ABI 4) Non-blocking: 1 when the device work of the submitted run has finished (so
  * _wait returns without waiting on the GPU), 0 while it runs, -ZFLAC_E_INVALID_ARGUMENT
- * without a submitted run, -ZFLAC_E_DEVICE on a device error. A caller with several batches
+ * without a submitted run, -ZFLAC_E_DEVICE on a device error. With ZFLAC_FLAG_DEVICE_MD5
+ * the run's hash counts as device work (a pending md5 hub launch is flushed when the hub is
+ * idle). A caller with several batches
  * in flight waits for whichever is ready instead of the oldest. */
 int zflac_hip_batch_ready(zflac_batch *b);
 /* Per-stream result of the last run: zflac error code, and shape when OK.

@@ -9,7 +9,8 @@
 #   tools/gpu.sh profile <tag> [bench args]   rocprofv3 --kernel-trace --stats of the bench
 #                                             workload: serial (one run in flight, the isolated
 #                                             launches the roofline uses) and three in flight
-#   tools/gpu.sh md5leg  <tag> <name> [args]  the decode+MD5 leg alone (MD5Q hardware queues, default 16)
+#   tools/gpu.sh md5leg  <tag> <name> [args]  the decode+MD5 leg alone (MD5Q hardware queues, default 7 =
+#                                             bench's 5 run + 2 md5 hub streams)
 #   tools/gpu.sh md5trace <tag>               rocprofv3 kernel trace of the decode+MD5 leg alone
 #   tools/gpu.sh pmc     <tag>                PMC passes (one rocprofv3 run per pass, counters only)
 #                                             + FETCH/WRITE calibration + summary (pmc_summary.json,
@@ -55,14 +56,14 @@ case $CMD in
     prof $O/serial python3 $R/bench.py --steps 20 --warmup 3 $QUIET --inflight 1 "$@" > $O/serial.log 2>&1 || exit $?
     prof $O/inflight3 python3 $R/bench.py --steps 20 --warmup 3 $QUIET "$@" > $O/inflight3.log 2>&1
     ;;
-  md5leg)  # md5leg <tag> <name> [bench args]: the decode+MD5 leg alone (16 hardware queues)
+  md5leg)  # md5leg <tag> <name> [bench args]: the decode+MD5 leg alone
     NAME=$1; shift
-    GPU_MAX_HW_QUEUES=${MD5Q:-16} timeout -k 10 300 python bench.py --md5-only --steps 36 --warmup 12 "$@" \
+    GPU_MAX_HW_QUEUES=${MD5Q:-7} timeout -k 10 300 python bench.py --md5-only --md5-steps 48 --warmup 12 "$@" \
         > $O/$NAME.json 2> $O/$NAME.err
     ;;
   md5trace)
-    export GPU_MAX_HW_QUEUES=${MD5Q:-16}  # as the bench's decode+MD5 child runs (set before rocprofv3, not via env)
-    prof $O/md5leg python3 $R/bench.py --md5-only --steps 24 --warmup 12 "$@" > $O/md5leg.log 2>&1
+    export GPU_MAX_HW_QUEUES=${MD5Q:-7}  # as the bench's decode+MD5 child runs (set before rocprofv3, not via env)
+    prof $O/md5leg python3 $R/bench.py --md5-only --md5-steps 36 --warmup 12 "$@" > $O/md5leg.log 2>&1
     ;;
   pmc)
     ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-md5 --no-e2e --inflight 1"
