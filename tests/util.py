@@ -76,6 +76,13 @@ PARITY_CONFIGS = {
     "stereo8_ls_packed": dict(channels=2, bps=8, stereo_mode=8, order=6, precision=7, block_size=2048,
                               n_samples=2048 * 4, noise_lsb=2.0, tone_amp=0.25),
     "stereo12_ms": dict(channels=2, bps=12, stereo_mode=10, order=4, block_size=1024, n_samples=1024 * 6),
+    # orders 9..12: the MB = 12 history bucket (16 history slots, 12 coefficients) of every container
+    "mono8_lpc10": dict(channels=1, bps=8, order=10, precision=7, block_size=2048, n_samples=2048 * 3 + 9,
+                        noise_lsb=1.0, tone_amp=0.3),
+    "mono16_lpc9": dict(channels=1, bps=16, order=9, precision=13, block_size=4096, n_samples=4096 * 2 + 77),
+    "stereo24_ls_lpc11": dict(channels=2, bps=24, stereo_mode=8, order=11, precision=14, block_size=4096,
+                              n_samples=4096 * 2 + 5),
+    "ch4_16_lpc12": dict(channels=4, bps=16, order=12, precision=13, block_size=2048, n_samples=2048 * 2 + 3),
     "ms20_lpc16_escape": dict(channels=2, bps=20, stereo_mode=10, order=16, precision=14, block_size=4096,
                               n_samples=4096 * 3, escape_every=7),
     "mono24_rice2": dict(channels=1, bps=24, order=8, block_size=4096, n_samples=4096 * 3, rice2=1),
