@@ -10,6 +10,10 @@
 //                   the host's sequential planner.
 #include "device_common.h"
 
+#ifndef ZFLAC_SCAN_AUX
+#define ZFLAC_SCAN_AUX 0  // cache policy bits of k_scan's loads (experiment: 2 = nontemporal)
+#endif
+
 namespace zflac {
 
 // ----------------------------------------------------------------------------------
@@ -88,7 +92,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
 #pragma unroll
     for (int r = 0; r < R; r++)
         v[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, threadIdx.x * 16u,
-                                                                                 r * SCAN_THREADS * 16, 0));
+                                                                                 r * SCAN_THREADS * 16, ZFLAC_SCAN_AUX));
     const StreamDesc S = a.streams[ch.stream];
     if (threadIdx.x == 0) {
         s_cnt = 0;
