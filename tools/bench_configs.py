@@ -141,8 +141,10 @@ def main():
             print(json.dumps(r), flush=True)
             rows.append(r)
     if a.out:
-        with open(a.out, "w") as f:
-            json.dump({"rows": rows}, f, indent=1)
+        import zflac_amd
+
+        with open(a.out, "w") as f:  # the loaded library's embedded build id (zflac_hip_build_id)
+            json.dump({"build_id": zflac_amd.build_id(), "lib": zflac_amd.lib_path, "rows": rows}, f, indent=1)
     if not all(r["bit_exact"] for r in rows):
         sys.exit(1)
 
