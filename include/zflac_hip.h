@@ -90,11 +90,10 @@ typedef struct zflac_timings {
     double host_md5_ms; /* last batch_read / read: host STREAMINFO MD5 (overlapped with the D2H) */
     double crc16_ms;    /* k_crc16 of the last run (ZFLAC_FLAG_CHECK_CRC16 with ZFLAC_FLAG_TIMING), else 0 */
     /* (ABI 4) synchronous `rest` decode launches of the last run: frame groups of a k_decode
-     * history bucket the batch's launch plan had not predicted (for a two-pass class: the
-     * class rerun on the walk path); the bucket is then added to the plan, so a later run of
-     * the same batch has none */
+     * history bucket the batch's launch plan had not predicted; the bucket is then added to
+     * the plan, so a later run of the same batch has none */
     uint32_t rest_launches;
-    uint32_t two_pass;      /* (ABI 4) classes of the last run decoded two-pass (no walk) */
+    uint32_t reserved0;
 } zflac_timings;
 
 typedef struct zflac_batch zflac_batch;

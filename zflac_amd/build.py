@@ -12,7 +12,6 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libzflac_hip.so")
 SOURCES = [os.path.join(CSRC, f"decode_k{k}_{lay}{mix}.hip") for k in (1, 2, 0) for lay in ("stereo", "mono", "multi")
            for mix in ("", "_mix")]
-SOURCES += [os.path.join(CSRC, f"decode_k1_{p}.hip") for p in ("s0", "s1")]  # two-pass stereo
 SOURCES += [os.path.join(CSRC, n) for n in ("scan.hip", "md5.hip", "crc16.hip", "walk_wave.hip", "host.cpp")]
 HEADERS = [os.path.join(CSRC, n) for n in ("common.h", "md5.hpp", "device_common.h", "decode.inc")]
 DEPS = SOURCES + HEADERS + [os.path.join(ROOT, "include", "zflac_hip.h")]

@@ -138,8 +138,6 @@ struct DecodeArgs {
     uint32_t rest;          // set on the `rest` launch (of the most general kernel, order 32 with
                             // constant / verbatim lanes) that decodes the frame groups of every
                             // bucket outside full_mask
-    int16_t* scratch;          // two-pass stereo (16-bit): channel 0's PCM, one row per frame
-    uint32_t scratch_stride;   // ... of scratch_stride samples (a multiple of 32 >= the largest block)
     uint32_t rest_only;     // host only: launch nothing but the rest kernel (no walk, no bucket
                             // kernels). The normal launch never includes it: the host issues it
                             // after a run whose order-8 launch reported a bucket outside

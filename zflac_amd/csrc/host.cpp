@@ -38,9 +38,6 @@ ZFLAC_DECL_LAUNCH(1)
 ZFLAC_DECL_LAUNCH(2)
 #undef ZFLAC_DECL_LAUNCH
 hipError_t launch_walk_wave(int kind, const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
-// two-pass stereo, 16-bit containers (decode_k1_s0.hip / decode_k1_s1.hip)
-hipError_t launch_decode_k1_s0(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
-hipError_t launch_decode_k1_s1(const DecodeArgs& a, uint32_t max_frames, hipStream_t st);
 
 // Which subframe-start walk a launch over `frames` frames of `nch` channels uses: k_walk
 // (lane per frame: 64 serial chains per wave, nch - 1 subframes each) needs tens of thousands
@@ -68,14 +65,6 @@ static hipError_t launch_decode(int kind, const DecodeArgs& a, uint32_t max_fram
                                 hipEvent_t mid = nullptr, hipStream_t front = nullptr, hipEvent_t join = nullptr,
                                 uint64_t est_frames = 0, int flags = 0) {
     const int lay = a.nch == 2 ? 2 : (a.nch == 1 ? 1 : 0);
-    if (kind == 1 && a.nch == 2 && a.scratch && !a.rest_only) {  // two-pass stereo: no walk
-        if (mid) {
-            const hipError_t e = hipEventRecord(mid, st);
-            if (e != hipSuccess) return e;
-        }
-        const hipError_t e = launch_decode_k1_s0(a, max_frames, st);
-        return e != hipSuccess ? e : launch_decode_k1_s1(a, max_frames, st);
-    }
     hipStream_t ws = front ? front : st;
     if (a.nch > 1 && !a.rest_only) {
         hipError_t e;
@@ -325,11 +314,6 @@ struct Class {
     // the first subframe of each member's first frame, at batch creation (plan_buckets)
     uint32_t full_mask = 0;
     bool redone = false;  // the last run re-ran the class (candidate table regrown)
-    // two-pass stereo decode (16-bit stereo classes whose predicted buckets are all pure): no
-    // walk; channel 0's PCM goes through `scratch` (scratch_stride samples per candidate frame)
-    bool two_pass = false;
-    uint32_t scratch_stride = 0;
-    DevBuf<int16_t> scratch;
     DevBuf<uint8_t> in;
     DevBuf<uint8_t> out;
     DevBuf<StreamDesc> d_desc;
@@ -568,22 +552,8 @@ uint32_t plan_buckets(const zflac_batch* b, const Class& C, const zflac_stream* 
     return mask;
 }
 
-// ZFLAC_TWO_PASS=0 / 1: the two-pass stereo decode off / on for 16-bit stereo classes
-// (read at batch creation)
-bool two_pass_enabled() {
-    const char* e = std::getenv("ZFLAC_TWO_PASS");
-    return e ? e[0] == '1' : false;
-}
-
 void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     C.full_mask = plan_buckets(b, C, src);
-    const uint32_t mix_bits = bucket_bit(8, true) | bucket_bit(32, true);
-    C.two_pass = two_pass_enabled() && C.kind == 1 && C.nch == 2 && C.full_mask && !(C.full_mask & mix_bits);
-    if (C.two_pass) {
-        uint32_t mb = 16;
-        for (uint32_t i : C.members) mb = std::max<uint32_t>(mb, b->streams[i].si.max_block ? b->streams[i].si.max_block : 65535u);
-        C.scratch_stride = (mb + 31) & ~31u;
-    }
     const int esz = esz_of_kind(C.kind);
     // input layout: each stream 16-byte aligned
     std::vector<uint64_t> in_off(C.members.size());
@@ -685,7 +655,6 @@ void alloc_candidates(Class& C) {
     C.c_err.alloc(C.cap);
     C.sub.alloc((size_t)C.cap * MAX_CH);
     C.group_mb.alloc((size_t)C.cap / 4 + 2);  // one per k_decode frame group (>= 8 frames each)
-    if (C.two_pass) C.scratch.alloc((size_t)C.cap * C.scratch_stride);
 }
 
 DecodeArgs decode_args(Class& C) {
@@ -750,10 +719,6 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     DecodeArgs da = decode_args(C);
     da.bucket_used = C.misc.p + 2;
     da.full_mask = C.full_mask;
-    if (C.two_pass) {
-        da.scratch = C.scratch.p;
-        da.scratch_stride = C.scratch_stride;
-    }
     ck(launch_decode(C.kind, da, std::min(C.grid_frames, C.cap), b->rs, timing_last ? b->ev[4] : nullptr,
                      b->front, b->front_join, C.est_frames, b->flags));
     st = b->rs;  // decode, verify and the read-backs
@@ -1228,16 +1193,7 @@ void finish_batch(zflac_batch* b) {
         // more candidates than the grids were sized for (false syncs): correct (the kernels
         // stride over them), but slower; size the next run's grids for them
         if (C.h_misc[0] > C.grid_frames) C.grid_frames = std::min(C.cap, C.h_misc[0] + C.h_misc[0] / 64 + 64);
-        if (C.two_pass && (C.h_misc[2] & ~C.full_mask)) {
-            // two-pass: a bucket without a launch (or constant / verbatim subframes) was used;
-            // this class decodes with the walk from now on, the launch set extended (rerun now)
-            C.two_pass = false;
-            C.full_mask |= C.h_misc[2] & BUCKET_MASK_ALL;
-            C.redone = true;
-            enqueue_class(b, C, false, false);
-            ck(hipStreamSynchronize(b->stream));
-            rest_launches++;
-        } else if (C.full_mask && (C.h_misc[2] & ~C.full_mask)) {  // a bucket without a launch was used
+        if (C.full_mask && (C.h_misc[2] & ~C.full_mask)) {  // a bucket without a launch was used
             enqueue_rest(b, C);
             C.redone = true;
             rest_launches++;
@@ -1354,8 +1310,6 @@ void finish_batch(zflac_batch* b) {
     b->timings.output_bytes = out_bytes;
     b->timings.samples = samples;
     b->timings.rest_launches = rest_launches;
-    b->timings.two_pass = 0;
-    for (auto& cp : b->classes) b->timings.two_pass += cp->two_pass ? 1u : 0u;
 }
 
 // MD5 of the decoded stream exactly as zflac hashes it: before left-justify, 24-bit
