@@ -180,6 +180,33 @@ def test_device_md5_cooperative_loads(gpu_ready, name, loads):
     b.close()
 
 
+@pytest.mark.parametrize("nohub", [False, True])
+def test_device_md5_hub_and_run_stream(gpu_ready, monkeypatch, nohub):
+    """Eight batches in flight, collected in completion order: through the md5 hub (several
+    runs per k_md5_coop launch, on hub streams), and with ZFLAC_MD5_NOHUB=1 (each run's hash
+    on its run stream, right behind its decode). Every digest equals STREAMINFO's, on
+    every run, and _ready turns 1 only once the hash has landed."""
+    if nohub:
+        monkeypatch.setenv("ZFLAC_MD5_NOHUB", "1")
+    sts = [synth.generate(**synth.config_c3(n_frames=4, seed=9100 + k)) for k in range(20)]
+    datas = [s.flac for s in sts]
+    bs = [zflac_amd.Batch(datas, device_md5=True, timing=True) for _ in range(8)]
+    for rnd in range(2):
+        for b in bs:
+            b.submit()
+        pending = set(range(len(bs)))
+        while pending:
+            for j in list(pending):
+                if bs[j].ready():
+                    bs[j].wait()
+                    pending.discard(j)
+                    for i, d in enumerate(datas):
+                        assert bs[j].info(i)[0] == 0, (rnd, j, i)
+                        assert bs[j].md5(i) == _streaminfo_md5(d), (rnd, j, i)
+    for b in bs:
+        b.close()
+
+
 def test_device_md5_c5_shard(gpu_ready):
     """C5-shaped members (32 frames, 131072 samples/ch), device MD5 against STREAMINFO."""
     streams = synth.generate_many([synth.config_c5(i) for i in range(130)])
