@@ -91,7 +91,8 @@ def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None, help="ranks (one per GPU); default WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--inflight", type=int, default=3, help="shard runs overlapped on the device (1 = serial)")
+    ap.add_argument("--inflight", type=int, default=4,
+                    help="shard runs overlapped on the device (1 = serial), on as many run streams")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--streams-per-gpu", type=int, default=STREAMS_PER_GPU)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample budget (all cores)")
@@ -389,7 +390,8 @@ def start_md5_child(args):
     if args.dry_run:
         cmd.append("--dry-run")
     q = args.md5_hw_queues or args.md5_run_streams + args.md5_hub_streams  # one hardware queue per stream
-    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(q))
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(q), ZFLAC_RUN_STREAMS=str(args.md5_run_streams),
+               ZFLAC_HUB_STREAMS=str(args.md5_hub_streams), ZFLAC_MD5_RUNS=str(args.md5_runs))
     return subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE)
 
 
@@ -450,6 +452,9 @@ def main():
     device = 0 if args.same_device else local_rank
     backend = args.backend or ("gloo" if (args.dry_run or args.same_device) else "nccl")
     md5_proc = None if args.no_md5 else start_md5_child(args)
+    # one run stream per run in flight (read by the library when it first uses the device;
+    # the HIP default of four hardware queues covers four run streams)
+    os.environ.setdefault("ZFLAC_RUN_STREAMS", str(max(1, args.inflight)))
     dist = None
     if world > 1:
         import torch
