@@ -8,7 +8,8 @@
 #   tools/gpu.sh bench   <tag> [bench args]   one bench line
 #   tools/gpu.sh profile <tag> [bench args]   rocprofv3 --kernel-trace --stats of the bench
 #                                             workload: serial (one run in flight, the isolated
-#                                             launches the roofline uses) and three in flight
+#                                             launches the roofline uses) and the bench's default
+#                                             runs in flight (four; round-4 profiles: three)
 #   tools/gpu.sh md5leg  <tag> <name> [args]  the decode+MD5 leg alone (MD5Q hardware queues, default 7 =
 #                                             bench's 5 run + 2 md5 hub streams)
 #   tools/gpu.sh md5trace <tag>               rocprofv3 kernel trace of the decode+MD5 leg alone
@@ -54,7 +55,7 @@ case $CMD in
     ;;
   profile)
     prof $O/serial python3 $R/bench.py --steps 20 --warmup 3 $QUIET --inflight 1 "$@" > $O/serial.log 2>&1 || exit $?
-    prof $O/inflight3 python3 $R/bench.py --steps 20 --warmup 3 $QUIET "$@" > $O/inflight3.log 2>&1
+    prof $O/inflight python3 $R/bench.py --steps 20 --warmup 3 $QUIET "$@" > $O/inflight.log 2>&1
     ;;
   md5leg)  # md5leg <tag> <name> [bench args]: the decode+MD5 leg alone
     NAME=$1; shift
