@@ -17,7 +17,8 @@ def load(path):
     rows = []
     for f in glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            rows.append({"name": r["Kernel_Name"].split("(")[0].replace("void ", ""),
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+            rows.append({"name": name.split("(")[0],
                          "start": int(r["Start_Timestamp"]), "end": int(r["End_Timestamp"]),
                          "queue": r.get("Queue_Id"), "stream": r.get("Stream_Id")})
     return rows
