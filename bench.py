@@ -6,9 +6,10 @@ Workload (BASELINE.json configs[4], per-GPU share; its codec parameters are conf
 LPC order 8 (synthetic, seeded per global stream index). One "step" = one batch run
 (zflac_hip_batch_submit + _wait) over the rank's whole shard: frame-sync scan, candidate
 compaction, subframe decode (Rice, LPC rollback, decorrelation, PCM pack-out) and chain
-verification, inputs already in HBM, outputs left in HBM. Three runs are kept in flight
-(--inflight 3, each with its own buffers and HIP stream), so one run's scan and walk
-overlap another's decode; `ms_per_step_serial` is the same shard one run at a time.
+verification, inputs already in HBM, outputs left in HBM. Four runs are kept in flight
+(--inflight 4, each with its own buffers; bench.py sets ZFLAC_RUN_STREAMS to --inflight so
+each run has a run stream of its own), so one run's scan and walk overlap another's decode;
+`ms_per_step_serial` is the same shard one run at a time.
 N GPUs = N ranks with disjoint shards (weak
 scaling, no collective in the data path; torch.distributed only for the timing barrier
 and the max over ranks).

@@ -132,6 +132,10 @@ int zflac_hip_batch_run(zflac_batch *b);
  * on a submitted batch and _wait without one return ZFLAC_E_INVALID_ARGUMENT, and results
  * (_info, _read, ...) are unavailable between the two. Destroying a submitted batch waits
  * for its kernels. */
+/* With ZFLAC_FLAG_DEVICE_MD5, _wait of a run whose hash is still queued in the md5 hub
+ * flushes the hub: one launch hashes every pending run (up to ZFLAC_MD5_RUNS) and waits on
+ * each of their decodes, so the digests of the waited run arrive with the slowest of those
+ * runs, and md5_ms reports that shared launch's time. */
 int zflac_hip_batch_submit(zflac_batch *b);
 int zflac_hip_batch_wait(zflac_batch *b);
 /* (ABI 4) Non-blocking: 1 when the device work of the submitted run has finished (so

@@ -344,6 +344,7 @@ struct Class {
 // Batch
 // ---------------------------------------------------------------------------------
 void hub_release_ext(zflac_batch* b);  // flush a run still pending in its device's md5 hub
+void hub_forget_ext(zflac_batch* b);   // drop a run from its device's md5 hub without hashing it
 }  // namespace zflac
 
 struct zflac_batch {
@@ -363,11 +364,14 @@ struct zflac_batch {
     // so that many batches in flight share a few hardware queues; `stream` (the batch's own)
     // carries the synchronous work (upload, regrowth, the sequential planner, read-backs)
     hipStream_t rs = nullptr;
-    // ZFLAC_FLAG_DEVICE_MD5 runs hash in the device's md5 hub (one k_md5_multi launch over
+    // ZFLAC_FLAG_DEVICE_MD5 runs hash in the device's md5 hub (one k_md5_coop launch over
     // the runs of several batches, on the hub's stream): ev_done then marks the decode only,
     // ev_md5 the hash and its digest read-back; md5_pending until the hub launched it
     hipEvent_t ev_md5 = nullptr;
-    bool md5_pending = false;
+    // written under the hub's lock, read without it by _ready / hub_release (other threads
+    // flush the hub from their own batches' submit / wait / ready)
+    std::atomic<bool> md5_pending{false};
+    bool md5_failed = false;  // the hub launch that held this run threw: its digests are void
     bool md5_hub = false;  // this run's hash goes through the hub
     bool have_timing = false;
     bool ran = false;        // results exist only after a completed batch_run / batch_wait
@@ -390,6 +394,10 @@ struct zflac_batch {
         if (md5_pending) {  // still in the md5 hub: flush it, then let the hash finish
             try {
                 zflac::hub_release_ext(this);
+            } catch (...) {
+            }
+            try {
+                zflac::hub_forget_ext(this);  // never leave a pointer to this batch in the hub
             } catch (...) {
             }
         }
@@ -467,10 +475,11 @@ Uploader& uploader(int device) {
 }
 
 // The device's run streams: every batch run (zflac_hip_batch_submit) goes to the next one
-// in turn, so any number of batches in flight use n_run (3) hardware queues (runs on one
-// stream execute in submit order; three in flight is where the C5 shard's throughput peaks).
-// Created before any batch's own stream, so that with HIP's default four hardware queues
-// (GPU_MAX_HW_QUEUES) the three run streams and the md5 hub stream each hold one of their own.
+// in turn, so any number of batches in flight use n_run (3 by default) hardware queues (runs
+// on one stream execute in submit order). bench.py keeps four runs in flight and sets
+// ZFLAC_RUN_STREAMS from its --inflight (four: 1-3 % faster than three since round 4).
+// Created before any batch's own stream, so that with enough hardware queues
+// (GPU_MAX_HW_QUEUES) the run streams and the md5 hub stream each hold one of their own.
 // ZFLAC_RUN_STREAMS / ZFLAC_HUB_STREAMS override the counts (at most 8 / 4).
 constexpr int MAX_RUN_STREAMS = 8;
 struct Md5Hub;
@@ -1048,7 +1057,7 @@ void finish_md5(zflac_batch* b, bool timing);
 // Hashing each run on its own batch stream made the decode+MD5 throughput the number of
 // batches in flight over (decode + hash latency), and each batch held a hardware queue for
 // its whole hash. The hub collects the DEVICE_MD5 runs whose decode has been enqueued and
-// hashes up to MD5_MAX_SEGS of them in ONE k_md5_multi launch on its own stream (waiting
+// hashes up to MD5_MAX_SEGS of them in ONE k_md5_coop launch on its own stream (waiting
 // on each run's decode event), so few launches and few hardware queues carry every chain.
 // A run is flushed into a launch once `runs` are pending, when its batch is waited on, or
 // when its batch polls _ready with its decode done and no hub launch in flight.
@@ -1062,6 +1071,22 @@ struct Md5Hub {
     bool any = false;
     std::vector<zflac_batch*> pend;
     uint32_t runs = 6;
+    int device = 0;  // the hub's launches and copies run with this device current
+};
+
+// Makes `dev` the calling thread's current device for a scope and restores the previous
+// one: hub flushes can be triggered from any batch's call (ready / wait / destroy), on a
+// thread whose current device is another one.
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) ck(hipSetDevice(dev));
+    }
+    ~DeviceScope() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
 };
 
 DeviceStreams::DeviceStreams() : hub_p(new Md5Hub()), hub(*hub_p) {
@@ -1079,7 +1104,10 @@ DeviceStreams& device_streams(int device) {
     static std::unordered_map<int, DeviceStreams*> per_device;  // never destroyed: outlives every batch
     std::lock_guard<std::mutex> lock(mu);
     DeviceStreams*& d = per_device[device];
-    if (!d) d = new DeviceStreams();
+    if (!d) {
+        d = new DeviceStreams();
+        d->hub.device = device;
+    }
     return *d;
 }
 
@@ -1091,9 +1119,27 @@ hipStream_t next_run_stream(int device) {
     return d.run[d.next++ % d.n_run];
 }
 
-// One launch over every pending run (caller holds hub.mu).
+// One launch over every pending run (caller holds hub.mu). Any exit, a throwing HIP call
+// included, leaves the hub empty: the runs of a launch that failed part way are marked
+// md5_failed (their wait reports DeviceError) instead of staying queued, so no later flush
+// can touch a batch destroyed in between.
+void hub_flush_runs(Md5Hub& h);
 void hub_flush(Md5Hub& h) {
     if (h.pend.empty()) return;
+    try {
+        DeviceScope dev(h.device);
+        hub_flush_runs(h);
+    } catch (...) {
+        for (zflac_batch* b : h.pend) {
+            if (b->md5_pending) b->md5_failed = true;
+            b->md5_pending = false;
+        }
+        h.pend.clear();
+        throw;
+    }
+}
+
+void hub_flush_runs(Md5Hub& h) {
     hipStream_t hs = h.st[h.next++ % h.n_st];
     Md5Segs sg;
     std::memset(&sg, 0, sizeof(sg));
@@ -1123,12 +1169,20 @@ void hub_flush(Md5Hub& h) {
     h.pend.clear();
 }
 
-// The run's hash launched (flushing the hub if it is still pending); true if it had to flush.
+// The run's hash launched (flushing the hub if it is still pending).
 void hub_release(zflac_batch* b) {
     if (!b->md5_pending) return;
     Md5Hub& h = md5_hub(b->device);
     std::lock_guard<std::mutex> lock(h.mu);
     if (b->md5_pending) hub_flush(h);
+}
+
+// Drop the run from the hub without hashing it (a failed submit or wait, a destroyed batch).
+void hub_forget(zflac_batch* b) {
+    Md5Hub& h = md5_hub(b->device);
+    std::lock_guard<std::mutex> lock(h.mu);
+    h.pend.erase(std::remove(h.pend.begin(), h.pend.end(), b), h.pend.end());
+    b->md5_pending = false;
 }
 
 // Phase 1 of a run: every class's parallel pipeline on the next of the device's run streams,
@@ -1176,6 +1230,10 @@ void finish_batch(zflac_batch* b) {
     b->rs = b->stream;  // from here on (regrowth, rest launch, planner): the batch's own stream
     if (b->md5_hub) {  // the run's hash (and its digests' read-back) in the md5 hub
         hub_release(b);
+        if (b->md5_failed) {
+            b->md5_failed = false;
+            throw DeviceError{};  // the md5 hub launch holding this run failed
+        }
         ck(hipEventSynchronize(b->ev_md5));
     }
     uint32_t rest_launches = 0;
@@ -1625,6 +1683,7 @@ int create_batch(const zflac_stream* streams, size_t n, int device, int flags, z
 }  // namespace
 
 void hub_release_ext(zflac_batch* b) { hub_release(b); }
+void hub_forget_ext(zflac_batch* b) { hub_forget(b); }
 }  // namespace zflac
 
 // ---------------------------------------------------------------------------------
@@ -1678,6 +1737,10 @@ int zflac_hip_batch_create(const zflac_stream* streams, size_t n, int device, in
 // ZFLAC_FRONT_PRIORITY, the front stream) may still use the candidate buffers a retry
 // reallocates.
 static void drain_failed_submit(zflac_batch* b) {
+    try {
+        hub_forget(b);
+    } catch (...) {
+    }
     (void)hipStreamSynchronize(b->stream);
     if (b->rs) (void)hipStreamSynchronize(b->rs);
     if (b->front) (void)hipStreamSynchronize(b->front);
@@ -1708,18 +1771,25 @@ int zflac_hip_batch_submit(zflac_batch* b) {
 int zflac_hip_batch_wait(zflac_batch* b) {
     if (!b || !b->submitted) return E_INVALID_ARGUMENT;
     b->submitted = false;
+    int rc = E_OK;
     try {
         finish_batch(b);
         b->timings.run_wall_ms = now_ms() - b->submit_t0;
         b->ran = true;
     } catch (const DeviceError&) {
-        return E_DEVICE;
+        rc = E_DEVICE;
     } catch (const std::bad_alloc&) {
-        return E_OUT_OF_MEMORY;
+        rc = E_OUT_OF_MEMORY;
     } catch (const std::exception&) {
-        return E_DEVICE;
+        rc = E_DEVICE;
     }
-    return E_OK;
+    if (rc != E_OK && b->md5_pending) {  // failed before the hub released this run
+        try {
+            hub_forget(b);
+        } catch (...) {
+        }
+    }
+    return rc;
 }
 
 int zflac_hip_batch_ready(zflac_batch* b) {

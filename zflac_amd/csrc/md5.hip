@@ -14,9 +14,10 @@
 //
 // A lane's time is its stream's chain (~4 dependent VALU ops per round), so a batch's hash
 // takes about as long as its longest stream, whatever the stream count. Runs are hashed by
-// the device's md5 hub (host.cpp): one k_md5_multi launch over the certified streams of
-// several runs, on a stream of its own, while the runs of other batches decode. A wave
-// reads its 64 streams' data cooperatively through LDS (hash_units_coop).
+// the device's md5 hub (host.cpp): one launch over the certified streams of several runs,
+// on a stream of its own, while the runs of other batches decode. That launch is k_md5_coop
+// (a wave reads its 64 streams' data cooperatively through LDS, hash_units_coop) when every
+// job shares one mode and 16-byte alignment, else k_md5_multi (each lane its own loads).
 #include <hip/hip_runtime.h>
 
 #include "common.h"
