@@ -1884,6 +1884,46 @@ extern "C" int zflac_hip_probe(zflac_batch* b, unsigned long long* out, int n) {
 }
 #endif
 
+#ifdef ZFLAC_REPLAY
+// Diagnostic build only (tools/replay.py): re-enqueue parts of each batch's last run `reps`
+// times, batch i on its own run stream, with no host work in between, and return the wall
+// time: what = 1 walk, 2 decode, 3 walk + decode, 4 the whole run (enqueue_class: fills, scan,
+// compact, walk, decode, verify, read-backs). Separates the device's throughput for each part
+// from the host side of submit / wait. Outputs are rewritten with the same values.
+extern "C" int zflac_hip_replay(zflac_batch** bs, int nb, int reps, int what, double* ms) {
+    try {
+        if (nb <= 0 || !bs || !ms) return E_INVALID_ARGUMENT;
+        ck(hipSetDevice(bs[0]->device));
+        for (int i = 0; i < nb; i++) {  // one run stream (hardware queue) per batch, as submit
+            ck(hipStreamSynchronize(bs[i]->rs));
+            bs[i]->rs = next_run_stream(bs[i]->device);
+        }
+        const double t0 = now_ms();
+        for (int r = 0; r < reps; r++) {
+            for (int i = 0; i < nb; i++) {
+                zflac_batch* b = bs[i];
+                Class& C = *b->classes[0];
+                if (what == 4) {
+                    enqueue_class(b, C, false, false);
+                    continue;
+                }
+                DecodeArgs da = decode_args(C);
+                da.full_mask = C.full_mask;
+                const uint32_t mf = std::min(C.grid_frames, C.cap);
+                if (what & 1) ck(launch_walk_k1(da, mf, b->rs));
+                if (what & 2) ck(launch_decode_k1_stereo(da, mf, b->rs));
+            }
+        }
+        for (int i = 0; i < nb; i++) ck(hipStreamSynchronize(bs[i]->rs));
+        *ms = now_ms() - t0;
+        for (int i = 0; i < nb; i++) bs[i]->rs = bs[i]->stream;
+        return E_OK;
+    } catch (const DeviceError&) {
+        return E_DEVICE;
+    }
+}
+#endif
+
 void zflac_hip_batch_destroy(zflac_batch* b) {
     if (!b) return;
     (void)hipSetDevice(b->device);
