@@ -59,6 +59,18 @@ __device__ __forceinline__ uint32_t sync_mask(uint32_t d, uint32_t dn) {
     return ff_mask(d) & zero;
 }
 
+// Nonzero iff some byte i of d is 0xFF and the byte after it 0xF8 / 0xF9: the same test as
+// sync_mask, as an existence test only. Byte i of t is zero exactly at a sync code, and
+// (t - 0x01..01) & ~t & 0x80..80 is nonzero iff t has a zero byte (the borrows can mark a
+// byte above a zero one, never create a mark without one). ~5 VALU per dword against
+// sync_mask's ~10: k_scan runs it on every window and the exact masks only where it fires
+// (a sync code, or a 0xFF 0xF8|F9 pair in the coded bits: ~1 in 7 wave-windows of 1 KiB).
+__device__ __forceinline__ uint32_t sync_any(uint32_t d, uint32_t dn) {
+    const uint32_t nxt = __builtin_amdgcn_alignbyte(dn, d, 1);
+    const uint32_t t = ~d | ((nxt & 0xFEFEFEFEu) ^ 0xF8F8F8F8u);
+    return (t - 0x01010101u) & ~t & 0x80808080u;
+}
+
 // (Call at wave-uniform points: DPP reads the neighbour lane's registers.)
 __device__ __forceinline__ uint32_t lane_above(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, true);  // wave_shl:1
@@ -108,11 +120,17 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
         // (DPP), except for lane 63 and past the chunk end (zeroed), where a sync code in
         // byte 15 reads its next byte from memory (rare)
         const uint32_t n0 = lane_above(v[r].x);
+        const bool nx_mem = (threadIdx.x & 63u) == 63u || ws + 16 >= ch.end;
+        // cheap existence test first: the exact masks below only run in waves where some lane
+        // may hold a sync code in this window (its last byte is tested against memory there)
+        const bool maybe = (sync_any(v[r].x, v[r].y) | sync_any(v[r].y, v[r].z) | sync_any(v[r].z, v[r].w) |
+                            sync_any(v[r].w, n0)) != 0 ||
+                           (nx_mem && (v[r].w >> 24) == 0xFFu);
+        if (!maybe || ws >= ch.end) continue;
         const uint32_t c0 = sync_mask(v[r].x, v[r].y), c1 = sync_mask(v[r].y, v[r].z),
                        c2 = sync_mask(v[r].z, v[r].w);
         uint32_t c3 = sync_mask(v[r].w, n0);
-        const bool nx_mem = (threadIdx.x & 63u) == 63u || ws + 16 >= ch.end;
-        if (nx_mem && (v[r].w >> 24) == 0xFFu && ws < ch.end)
+        if (nx_mem && (v[r].w >> 24) == 0xFFu)
             c3 = (c3 & 0x00808080u) | ((a.in[ws + 16] & 0xFEu) == 0xF8u ? 0x80000000u : 0u);
         if ((c0 | c1 | c2 | c3) == 0 || ws >= ch.end) continue;  // no sync code: the common case
         uint32_t cand = (c0 * 0x00204081u) >> 28 & 15u;  // bit b: a sync code at byte b
