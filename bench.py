@@ -107,7 +107,7 @@ def parse_args():
                     help="decode+MD5 leg: the library's run streams (ZFLAC_RUN_STREAMS)")
     ap.add_argument("--md5-hub-streams", type=int, default=2,
                     help="decode+MD5 leg: md5 hub streams (ZFLAC_HUB_STREAMS), each launch hashing --md5-runs runs")
-    ap.add_argument("--md5-runs", type=int, default=6, help="decode+MD5 leg: runs per md5 hub launch (ZFLAC_MD5_RUNS)")
+    ap.add_argument("--md5-runs", type=int, default=8, help="decode+MD5 leg: runs per md5 hub launch (ZFLAC_MD5_RUNS)")
     ap.add_argument("--md5-hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES of the decode+MD5 leg's process (default: run + hub streams)")
     ap.add_argument("--sched", choices=["rr", "ready"], default="rr",

@@ -1070,7 +1070,7 @@ struct Md5Hub {
     hipEvent_t last = nullptr;  // behind the newest hub launch
     bool any = false;
     std::vector<zflac_batch*> pend;
-    uint32_t runs = 6;
+    uint32_t runs = 8;
     int device = 0;  // the hub's launches and copies run with this device current
 };
 

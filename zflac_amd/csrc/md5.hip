@@ -20,6 +20,9 @@
 // job shares one mode and 16-byte alignment, else k_md5_multi (each lane its own loads).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace zflac {
@@ -110,6 +113,15 @@ __device__ uint32_t message_byte(const Md5Job& j, uint64_t v) {
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// The wave's tile is its own (a workgroup holds several waves, each with a tile): the LDS
+// writes of all its lanes before any lane's reads, and the reads before the next writes.
+// LDS operations of one wave complete in order; the fence keeps the compiler's order and
+// waits for the wave's outstanding LDS operations.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
 constexpr int UNIT_WORDS = 64;  // raw dwords per unit: 4 blocks, or 3 blocks of 24-bit samples
 
 // Compress one unit (UNIT_WORDS raw dwords, plus the dword after it for unaligned bases).
@@ -241,7 +253,7 @@ __device__ __forceinline__ uint64_t hash_units_coop(const Md5Job& j, bool act, u
     for (uint32_t u = 0; u < maxu; u++) {
 #pragma unroll
         for (int i = 0; i < 16; i++) tile[i * 64 + L] = R[i];  // row 4i + L/16, slot L & 15
-        __syncthreads();
+        wave_sync();
         if (u + 1 < maxu) load(u + 1);
         if (u < nu) {
             if constexpr (MODE == MD5_S24) {
@@ -268,7 +280,7 @@ __device__ __forceinline__ uint64_t hash_units_coop(const Md5Job& j, bool act, u
                 }
             }
         }
-        __syncthreads();  // every lane's reads of the tile before the next unit's writes
+        wave_sync();  // every lane's reads of the tile before the next unit's writes
     }
     return (uint64_t)nu * MSG_PER_UNIT;
 }
@@ -355,12 +367,22 @@ __global__ __launch_bounds__(64) void k_md5_multi(Md5Segs sg) {
 // Every job of the launch in mode MODE with 16-byte aligned samples (the host checks):
 // the wave's lanes load cooperatively (hash_units_coop); lanes past the job list, or whose
 // stream this run did not certify, only help load.
+// Workgroups of ZFLAC_MD5_WG_WAVES waves (1..8, default 4), one 16 KiB tile each: the
+// workgroup's LDS decides how the hash shares CUs with k_decode, whose four 40 KiB
+// workgroups fill a CU's 160 KiB. A one-wave hash workgroup (16 KiB) on a CU leaves room
+// for three decode workgroups, so hash waves spread one per CU each cost that CU a quarter
+// of its decode capacity; four waves (64 KiB: one per SIMD, beside two decode workgroups)
+// put the same hash on a quarter as many CUs. Decode + MD5 on the C5 shard
+// (profiles/r5_md5_wg_sweep.json): 1 wave 357k, 2 366k, 3 383k, 4 401-428k, 5-8 290-300k
+// Msamples/s (five or more hash waves per CU starve the hash chains of issue slots).
+constexpr int MD5_MAX_WG_WAVES = 8;
+extern __shared__ u32x4 g_md5_tile[];
 template <int MODE>
-__global__ __launch_bounds__(64) void k_md5_coop(Md5Segs sg) {
-    __shared__ u32x4 tile[64 * 16];
+__global__ __launch_bounds__(64 * MD5_MAX_WG_WAVES) void k_md5_coop(Md5Segs sg) {
+    u32x4* const tile = g_md5_tile + (threadIdx.x >> 6) * (64 * 16);
     md5_prio();
     uint32_t* out = nullptr;
-    const Md5Job* jp = seg_job(sg, blockIdx.x * 64 + threadIdx.x, out);
+    const Md5Job* jp = seg_job(sg, blockIdx.x * blockDim.x + threadIdx.x, out);
     Md5Job j{};
     if (jp) j = *jp;
     const bool act = jp && !(j.status && *j.status);
@@ -376,18 +398,53 @@ __global__ __launch_bounds__(64) void k_md5_coop(Md5Segs sg) {
 
 }  // namespace
 
+// waves per k_md5_coop workgroup (ZFLAC_MD5_WG_WAVES, default MD5_WG_WAVES_DEFAULT)
+#ifndef MD5_WG_WAVES_DEFAULT
+#define MD5_WG_WAVES_DEFAULT 4
+#endif
+int md5_wg_waves() {
+    static const int w = [] {
+        const char* e = std::getenv("ZFLAC_MD5_WG_WAVES");
+        const int v = e ? atoi(e) : MD5_WG_WAVES_DEFAULT;
+        return v < 1 ? 1 : (v > MD5_MAX_WG_WAVES ? MD5_MAX_WG_WAVES : v);
+    }();
+    return w;
+}
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per device and kernel (the attribute
+// belongs to the kernel's instance on the current device)
+template <int MODE>
+hipError_t allow_md5_lds(size_t bytes) {
+    static std::atomic<uint64_t> done{0};
+    int dev = 0;
+    if (const hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done.load(std::memory_order_acquire) & bit) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_md5_coop<MODE>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) done.fetch_or(bit, std::memory_order_acq_rel);
+    return e;
+}
+
+template <int MODE>
+hipError_t launch_coop(const Md5Segs& sg, uint32_t n, hipStream_t st) {
+    const uint32_t w = (uint32_t)md5_wg_waves();
+    const size_t lds = (size_t)w * 64 * 16 * sizeof(u32x4);
+    if (const hipError_t e = allow_md5_lds<MODE>(lds); e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_md5_coop<MODE>, dim3((n + 64 * w - 1) / (64 * w)), dim3(64 * w), lds, st, sg);
+    return hipGetLastError();
+}
+
 hipError_t launch_md5_multi(const Md5Segs& sg, hipStream_t st, int coop_mode) {
     const uint32_t n = sg.start[sg.nseg];
     if (!n) return hipSuccess;
-    const dim3 g((n + 63) / 64), b(64);
     switch (coop_mode) {
-        case MD5_RAW: hipLaunchKernelGGL(k_md5_coop<MD5_RAW>, g, b, 0, st, sg); break;
-        case MD5_S16_SHIFT: hipLaunchKernelGGL(k_md5_coop<MD5_S16_SHIFT>, g, b, 0, st, sg); break;
-        case MD5_S32_SHIFT: hipLaunchKernelGGL(k_md5_coop<MD5_S32_SHIFT>, g, b, 0, st, sg); break;
-        case MD5_S24: hipLaunchKernelGGL(k_md5_coop<MD5_S24>, g, b, 0, st, sg); break;
-        default: hipLaunchKernelGGL(k_md5_multi, g, b, 0, st, sg); break;
+        case MD5_RAW: return launch_coop<MD5_RAW>(sg, n, st);
+        case MD5_S16_SHIFT: return launch_coop<MD5_S16_SHIFT>(sg, n, st);
+        case MD5_S32_SHIFT: return launch_coop<MD5_S32_SHIFT>(sg, n, st);
+        case MD5_S24: return launch_coop<MD5_S24>(sg, n, st);
+        default: hipLaunchKernelGGL(k_md5_multi, dim3((n + 63) / 64), dim3(64), 0, st, sg); return hipGetLastError();
     }
-    return hipGetLastError();
 }
 
 hipError_t launch_md5(const Md5Job* jobs, uint32_t n_jobs, uint32_t* digests, hipStream_t st, int coop_mode) {
