@@ -9,7 +9,9 @@ compaction, subframe decode (Rice, LPC rollback, decorrelation, PCM pack-out) an
 verification, inputs already in HBM, outputs left in HBM. Four runs are kept in flight
 (--inflight 4, each with its own buffers; bench.py sets ZFLAC_RUN_STREAMS to --inflight so
 each run has a run stream of its own), so one run's scan and walk overlap another's decode;
-`ms_per_step_serial` is the same shard one run at a time.
+`ms_per_step_serial` is the same shard one run at a time; that serial leg runs before the
+warm-up and the timed steps (the device ramps its clock up from idle over ~10-20 ms of load;
+`pre_timed_runs` in the JSON line) and gives the isolated kernel times from its second half.
 N GPUs = N ranks with disjoint shards (weak
 scaling, no collective in the data path; torch.distributed only for the timing barrier
 and the max over ranks).
@@ -555,6 +557,24 @@ def main():
             if pending[j]:
                 done(j)
 
+    # The serial leg first: the same shard one run at a time (no overlap), `steps` runs, for
+    # the isolated kernel times the roofline uses and the serial step time. It runs before the
+    # warm-up and the timed steps because the device leaves idle at a lower clock: after an
+    # idle gap, the first ~10 ms of load run slower (tools/warm_test.py,
+    # profiles/r5_warm_test.json: 20-step stretches at 0.53 ms/step right after 5 warm-up
+    # runs, 0.47-0.49 once the device has been busy ~20 ms, 0.55-0.57 after a 50-500 ms
+    # idle gap). The isolated times come from the leg's second half, where the clock has
+    # settled (and `ms_per_step_serial` from the same half). The timed steps are unchanged:
+    # `warmup` runs, a barrier, `steps` runs.
+    serial = None
+    rec = None
+    if n_inf > 1:
+        half = args.steps // 2
+        run_steps(half, batches[:1])
+        rec = {n: [] for n in STAGES}
+        t1 = time.perf_counter()
+        run_steps(args.steps - half, batches[:1], rec)
+        serial = (time.perf_counter() - t1) / (args.steps - half)
     run_steps(args.warmup, batches)
     progress("warm-up done")
     barrier_sync()
@@ -566,16 +586,8 @@ def main():
     tm = batches[0].timings()
     samples_rank = tm.samples
     in_bytes, out_bytes = tm.input_bytes, tm.output_bytes
-
-    # the same shard one run at a time (no overlap): the isolated kernel times the roofline
-    # uses, and the serial step time for reference
-    serial = None
-    rec = rec_ov
-    if n_inf > 1:
-        rec = {n: [] for n in STAGES}
-        t1 = time.perf_counter()
-        run_steps(args.steps, batches[:1], rec)
-        serial = (time.perf_counter() - t1) / args.steps
+    if rec is None:
+        rec = rec_ov
     scan_ms, walk_ms, dec_ms, ver_ms = (rec[n] for n in STAGES)
 
     progress(f"timed steps done ({elapsed / args.steps * 1e3:.3f} ms/step)")
@@ -636,6 +648,9 @@ def main():
             "ms_per_step": round(ms_step, 4),
             "inflight": n_inf,
             "ms_per_step_serial": round(serial * 1e3, 4) if serial else None,
+            "pre_timed_runs": {"serial_leg": args.steps if serial else 0, "warmup": args.warmup,
+                               "why": "the serial leg (one run at a time, isolated kernel times) runs before the "
+                                      "warm-up: the device leaves idle at a lower clock (profiles/r5_warm_test.json)"},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
