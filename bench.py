@@ -93,7 +93,9 @@ def progress(msg: str) -> None:
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None, help="ranks (one per GPU); default WORLD_SIZE or 1")
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100,
+                    help="timed steps; 100 by default so that the four-run pipeline's fill and drain "
+                         "(about one step) are amortized (20 steps: ~4 %% lower, profiles/r5_steps_sweep.json)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="shard runs overlapped on the device (1 = serial), on as many run streams")
     ap.add_argument("--warmup", type=int, default=3)
