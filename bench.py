@@ -384,8 +384,8 @@ def start_md5_child(args):
     """Start the process that will run md5_leg (same rank, same shard) with GPU_MAX_HW_QUEUES
     set, so the headline's process keeps the runtime's defaults. Started before this process
     touches the GPU (no fork / exec from a process with a GPU context). It does not generate
-    anything: it blocks on its stdin until md5_leg_in_child sends it this rank's shard. Per
-    rank that is two processes (this one and the child) and host_threads(world) host threads."""
+    anything: it blocks on its stdin until md5_leg_in_child sends it this rank's shard. Started
+    by rank 0 only: world + 1 processes in all, each with host_threads(world) host threads."""
     cmd = [sys.executable, os.path.abspath(__file__), "--md5-leg-child", "--steps", str(args.steps), "--warmup",
            str(args.warmup), "--streams-per-gpu", str(args.streams_per_gpu), "--md5-inflight", str(args.md5_inflight),
            "--md5-steps", str(args.md5_steps), "--md5-run-streams", str(args.md5_run_streams),
@@ -456,7 +456,9 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     device = 0 if args.same_device else local_rank
     backend = args.backend or ("gloo" if (args.dry_run or args.same_device) else "nccl")
-    md5_proc = None if args.no_md5 else start_md5_child(args)
+    # the decode+MD5 leg (reported for rank 0 only) runs on rank 0 alone: at world 8 that is 9
+    # processes on the node instead of 16, the other ranks' GPUs idle meanwhile
+    md5_proc = None if (args.no_md5 or rank != 0) else start_md5_child(args)
     # one run stream per run in flight (read by the library when it first uses the device;
     # the HIP default of four hardware queues covers four run streams)
     os.environ.setdefault("ZFLAC_RUN_STREAMS", str(max(1, args.inflight)))
@@ -495,7 +497,7 @@ def main():
         tot = aggregate(dist, coll_dev, el, samples, sum(len(s) for s in streams), samples * 2, 0)
         digest = hashlib.sha256(b"".join(streams)).hexdigest()[:16]
         child = md5_leg_in_child(md5_proc, streams) if md5_proc is not None else None
-        # per rank: this process, its decode+MD5 child, and the host threads it may use
+        # per rank: this process, its decode+MD5 child (rank 0 only), and the host threads it may use
         rng = shard_range(rank, world, args.streams_per_gpu)
         mine = {"rank": rank, "shard": [rng.start, rng.stop], "pid": os.getpid(), "processes": 1 + (child is not None),
                 "host_threads": host_threads(world),
@@ -609,7 +611,7 @@ def main():
     # ZFLAC_FLAG_DEVICE_MD5, in a child process of its own whose GPU_MAX_HW_QUEUES covers
     # one hardware queue per batch in flight (md5_leg)
     md5 = None
-    if not args.no_md5:
+    if md5_proc is not None:
         batch.close()
         batch = None
         progress("verification done; decode+MD5 leg")

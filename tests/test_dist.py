@@ -134,13 +134,15 @@ def test_bench_self_launch_dry_run():
 
 def test_bench_self_launch_dry_run_world8():
     """The driver's 8-GPU shape, rehearsed on the CPU: `bench.py --gpus 8 --dry-run` starts 8
-    ranks, each with its decode+MD5 child, which receives the rank's shard over a pipe (it
-    does not regenerate it); host threads are the job's cores split over the ranks."""
+    ranks; rank 0 also starts its decode+MD5 child (the leg is reported for rank 0 only), which
+    receives the rank's shard over a pipe (it does not regenerate it); host threads are the
+    job's cores split over the ranks."""
     d = _bench("--gpus", "8", "--dry-run", "--streams-per-gpu", "2", "--steps", "1", "--warmup", "0", timeout=600)
     assert d["n_gpus"] == 8 and len(d["ranks"]) == 8
     assert d["shards"] == [[2 * r, 2 * r + 2] for r in range(8)]
-    assert all(r["child_got_shard"] and r["processes"] == 2 for r in d["ranks"])
-    assert d["processes_total"] == 16
+    assert d["ranks"][0]["child_got_shard"] and d["ranks"][0]["processes"] == 2
+    assert all(r["processes"] == 1 for r in d["ranks"][1:])
+    assert d["processes_total"] == 9
     assert d["host_threads_total"] <= max(8, d["host_cores"])
     print("per-rank processes", [r["processes"] for r in d["ranks"]], "host threads",
           [r["host_threads"] for r in d["ranks"]], "cores", d["host_cores"])
