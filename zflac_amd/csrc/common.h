@@ -90,6 +90,11 @@ struct ScanArgs {
     unsigned long long* chunk_units;  // sum of block_size*channels per chunk
     uint64_t* chunk_slots;      // CHUNK_CAP positions per chunk
     uint32_t* chunk_slot_units; // CHUNK_CAP units per chunk
+    // the run's per-stream status words and its 4 counters, zeroed by k_scan (instead of two
+    // fill launches per run); k_verify and later kernels of the run accumulate into them
+    uint32_t* status;
+    uint32_t n_status;
+    uint32_t* misc;
 };
 
 struct CompactArgs {

@@ -694,8 +694,10 @@ DecodeArgs decode_args(Class& C) {
 void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last) {
     hipStream_t st = b->front ? b->front : b->rs;  // scan, compact (and the walk) there
     const uint32_t nch = (uint32_t)C.chunks.size();
-    ck(hipMemsetAsync(C.status.p, 0, C.members.size() * sizeof(uint32_t), st));
-    ck(hipMemsetAsync(C.misc.p, 0, 4 * sizeof(uint32_t), st));
+    if (nch == 0) {  // (k_scan zeroes them otherwise)
+        ck(hipMemsetAsync(C.status.p, 0, C.members.size() * sizeof(uint32_t), st));
+        ck(hipMemsetAsync(C.misc.p, 0, 4 * sizeof(uint32_t), st));
+    }
     if (timing_first) ck(hipEventRecord(b->ev[0], st));
     ScanArgs sa;
     sa.in = C.in.p;
@@ -706,6 +708,9 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     sa.chunk_units = C.chunk_units.p;
     sa.chunk_slots = C.chunk_slots.p;
     sa.chunk_slot_units = C.chunk_slot_units.p;
+    sa.status = C.status.p;
+    sa.n_status = (uint32_t)C.members.size();
+    sa.misc = C.misc.p;
     ck(launch_scan(sa, st));
     if (nch) ck(launch_scan_chunks(C.chunk_cnt.p, C.chunk_units.p, nch, C.chunk_off.p, C.chunk_uoff.p, C.misc.p, st));
     CompactArgs ca;

@@ -87,6 +87,10 @@ __device__ __forceinline__ uint32_t lane_above(uint32_t v) {
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     const uint32_t chunk = blockIdx.x;
     if (chunk >= a.n_chunks) return;
+    // the run's status words and counters start at zero (read by kernels after this one)
+    for (uint32_t i = chunk * SCAN_THREADS + threadIdx.x; i < a.n_status; i += a.n_chunks * SCAN_THREADS)
+        a.status[i] = 0;
+    if (chunk == 0 && threadIdx.x < 4) a.misc[threadIdx.x] = 0;
     __shared__ uint32_t s_cnt;
     __shared__ unsigned long long s_units;
     __shared__ uint64_t s_pos[CHUNK_CAP];
