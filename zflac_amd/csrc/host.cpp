@@ -318,7 +318,8 @@ struct Class {
     DevBuf<uint8_t> out;
     DevBuf<StreamDesc> d_desc;
     DevBuf<ChunkDesc> d_chunks;
-    DevBuf<uint32_t> chunk_cnt, chunk_off, chunk_slot_units, misc, status;
+    DevBuf<uint32_t> chunk_cnt, chunk_off, chunk_slot_units, misc;  // misc: 4 counters, then `status`
+    uint32_t* status = nullptr;  // per-member status words, misc.p + 4 (one read-back for both)
     DevBuf<unsigned long long> chunk_units, chunk_uoff;
     DevBuf<uint64_t> chunk_slots;
     DevBuf<uint64_t> c_pos, c_out, c_end;
@@ -641,9 +642,9 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     C.chunk_slot_units.alloc(nc * CHUNK_CAP);
     C.chunk_off.alloc(nc + 1);
     C.chunk_uoff.alloc(nc + 1);
-    C.misc.alloc(4);
+    C.misc.alloc(4 + C.members.size());
+    C.status = C.misc.p + 4;
     C.dummy.alloc(DUMMY_BYTES + PROBE_BYTES);
-    C.status.alloc(C.members.size());
     ck(hipHostMalloc(reinterpret_cast<void**>(&C.pin.p), (4 + C.members.size()) * sizeof(uint32_t),
                      hipHostMallocDefault));
     std::memset(C.pin.p, 0, (4 + C.members.size()) * sizeof(uint32_t));
@@ -694,10 +695,8 @@ DecodeArgs decode_args(Class& C) {
 void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last) {
     hipStream_t st = b->front ? b->front : b->rs;  // scan, compact (and the walk) there
     const uint32_t nch = (uint32_t)C.chunks.size();
-    if (nch == 0) {  // (k_scan zeroes them otherwise)
-        ck(hipMemsetAsync(C.status.p, 0, C.members.size() * sizeof(uint32_t), st));
-        ck(hipMemsetAsync(C.misc.p, 0, 4 * sizeof(uint32_t), st));
-    }
+    if (nch == 0)  // (k_scan zeroes them otherwise)
+        ck(hipMemsetAsync(C.misc.p, 0, (4 + C.members.size()) * sizeof(uint32_t), st));
     if (timing_first) ck(hipEventRecord(b->ev[0], st));
     ScanArgs sa;
     sa.in = C.in.p;
@@ -708,7 +707,7 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     sa.chunk_units = C.chunk_units.p;
     sa.chunk_slots = C.chunk_slots.p;
     sa.chunk_slot_units = C.chunk_slot_units.p;
-    sa.status = C.status.p;
+    sa.status = C.status;
     sa.n_status = (uint32_t)C.members.size();
     sa.misc = C.misc.p;
     ck(launch_scan(sa, st));
@@ -750,11 +749,11 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     va.c_err = C.c_err.p;
     va.c_info = C.c_info.p;
     va.c_rate = C.c_rate.p;
-    va.status = C.status.p;
+    va.status = C.status;
     ck(launch_verify(va, C.cap, st));
     if (timing_last) ck(hipEventRecord(b->ev[3], st));
-    ck(hipMemcpyAsync(C.h_status, C.status.p, C.members.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    ck(hipMemcpyAsync(C.h_misc, C.misc.p, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    // the counters and the status words in one read-back (contiguous on both sides)
+    ck(hipMemcpyAsync(C.h_misc, C.misc.p, (4 + C.members.size()) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
 }
 
 // After a run whose order-8 launch found frame groups of a bucket the host did not
@@ -766,7 +765,7 @@ void enqueue_rest(zflac_batch* b, Class& C) {
     da.full_mask = C.full_mask;
     da.rest_only = 1;
     ck(launch_decode(C.kind, da, std::min(C.grid_frames, C.cap), st));
-    ck(hipMemsetAsync(C.status.p, 0, C.members.size() * sizeof(uint32_t), st));
+    ck(hipMemsetAsync(C.status, 0, C.members.size() * sizeof(uint32_t), st));
     VerifyArgs va;
     va.streams = C.d_desc.p;
     va.n_streams = (uint32_t)C.members.size();
@@ -780,9 +779,9 @@ void enqueue_rest(zflac_batch* b, Class& C) {
     va.c_err = C.c_err.p;
     va.c_info = C.c_info.p;
     va.c_rate = C.c_rate.p;
-    va.status = C.status.p;
+    va.status = C.status;
     ck(launch_verify(va, C.cap, st));
-    ck(hipMemcpyAsync(C.h_status, C.status.p, C.members.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    ck(hipMemcpyAsync(C.h_status, C.status, C.members.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     ck(hipStreamSynchronize(st));
 }
 
@@ -1537,7 +1536,7 @@ void plan_md5_pipeline(zflac_batch* b) {
         for (size_t m = 0; m < C.members.size(); m++) {
             const StreamDesc& D = C.desc[m];
             if (!D.valid_total) continue;
-            jobs.push_back(md5_job(b->streams[C.members[m]], C.out.p + D.out_base * esz, D.total, C.status.p + m));
+            jobs.push_back(md5_job(b->streams[C.members[m]], C.out.p + D.out_base * esz, D.total, C.status + m));
             who.push_back(C.members[m]);
         }
     }
