@@ -207,6 +207,39 @@ def test_device_md5_hub_and_run_stream(gpu_ready, monkeypatch, nohub):
         b.close()
 
 
+@pytest.mark.parametrize("via_ready", [False, True])
+def test_md5_hub_failed_launch_does_not_poison_next_run(gpu_ready, monkeypatch, via_ready):
+    """A failed md5 hub launch (fault injected with ZFLAC_FAULT_HUB_FLUSH=1) fails that run
+    with DeviceError, through _wait or through _ready; the batch's next run succeeds, with every
+    digest equal to STREAMINFO's (round-5 advisor finding: the failure flag leaked into the next
+    run, whose good results then read as DeviceError)."""
+    sts = [synth.generate(**synth.config_c3(n_frames=4, seed=9300 + k)) for k in range(6)]
+    datas = [s.flac for s in sts]
+    b = zflac_amd.Batch(datas, device_md5=True)
+    monkeypatch.setenv("ZFLAC_FAULT_HUB_FLUSH", "1")
+    b.submit()
+    if via_ready:
+        import time
+
+        t0 = time.time()
+        with pytest.raises(errors.DeviceError):
+            while not b.ready():  # ready() launches the pending hash itself: the flush fails there
+                assert time.time() - t0 < 60
+                time.sleep(0.001)
+        with pytest.raises(errors.DeviceError):
+            b.ready()  # still failed, never "finished"
+    with pytest.raises(errors.DeviceError):
+        b.wait()
+    monkeypatch.delenv("ZFLAC_FAULT_HUB_FLUSH")
+    for _ in range(2):
+        b.run()
+        for i, d in enumerate(datas):
+            assert b.info(i)[0] == 0, i
+            assert b.md5(i) == _streaminfo_md5(d), i
+            np.testing.assert_array_equal(b.read(i).samples.values, expected_samples(sts[i]))
+    b.close()
+
+
 def test_device_md5_c5_shard(gpu_ready):
     """C5-shaped members (32 frames, 131072 samples/ch), device MD5 against STREAMINFO."""
     streams = synth.generate_many([synth.config_c5(i) for i in range(130)])

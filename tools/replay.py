@@ -19,15 +19,20 @@ from zflac_amd import _lib  # noqa: E402
 
 streams = [s.flac for s in synth.generate_many([synth.config_c5(i) for i in range(1250)])]
 bs = [zflac_amd.Batch(streams) for _ in range(nb)]
-for b in bs:
-    b.run()
+if not os.environ.get("REPLAY_NORUN"):  # (scan-ablation variants: front parts only, no real run)
+    for b in bs:
+        b.run()
 L = _lib.load()
 fn = L.zflac_hip_replay
 fn.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                ctypes.POINTER(ctypes.c_double)]
 arr = (ctypes.c_void_p * nb)(*[b._h.value if hasattr(b._h, "value") else b._h for b in bs])
 out = {"inflight": nb, "reps": reps}
-for what, name in ((1, "walk"), (2, "decode"), (3, "walk+decode"), (4, "run")):
+parts = ((1, "walk"), (2, "decode"), (3, "walk+decode"), (4, "run"), (8, "scan"), (16, "front"))
+only = os.environ.get("REPLAY_PARTS")  # e.g. "scan,front3"
+for what, name in parts:
+    if only and name not in only.split(","):
+        continue
     ms = ctypes.c_double()
     fn(arr, nb, 2, what, ctypes.byref(ms))  # warm
     rc = fn(arr, nb, reps, what, ctypes.byref(ms))

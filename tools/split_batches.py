@@ -1,6 +1,6 @@
 """Steps over the C5 shard decoded as S sub-batches per step (1250/S streams each), with
 inflight*S sub-batches in flight, round robin: ms per step (whole shard) at K steps.
-Usage: python tools/split_test.py K S inflight [reps]"""
+Usage: python tools/split_batches.py K S inflight [reps]"""
 import os
 import sys
 import time

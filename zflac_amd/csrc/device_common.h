@@ -61,6 +61,41 @@ constexpr Crc8Table make_crc8_table() {  // x^8 + x^2 + x + 1, init 0 (RFC 9639 
 }
 static __constant__ Crc8Table CRC8 = make_crc8_table();
 
+// a (a polynomial of degree < 32 over GF(2)) mod x^8 + x^2 + x + 1. With x^8 = x^2 + x + 1,
+// a = t x^8 + l reduces to t (x^2 + x + 1) + l: one fold lowers the degree by 6, four take
+// 31 down to 7. Register-only: a table lookup is an LDS round trip per byte, and the bytes of
+// a header are a dependent chain.
+constexpr uint32_t crc8_reduce(uint32_t a) {
+    for (int i = 0; i < 4; i++) {
+        const uint32_t t = a >> 8;
+        a = (t ^ (t << 1) ^ (t << 2)) ^ (a & 0xFFu);
+    }
+    return a;
+}
+// CRC-8 (init 0, MSB first) after three more bytes b0 b1 b2 (w = b0 << 16 | b1 << 8 | b2):
+// the message (b0 ^ crc) x^16 + b1 x^8 + b2, times x^8, mod the polynomial
+constexpr uint32_t crc8_3(uint32_t crc, uint32_t w) { return crc8_reduce((w ^ (crc << 16)) << 8); }
+constexpr uint32_t crc8_1(uint32_t crc, uint32_t b) { return crc8_reduce((crc ^ b) << 8); }
+constexpr bool crc8_fold_matches_table() {
+    const Crc8Table t = make_crc8_table();
+    for (uint32_t i = 0; i < 256; i++)
+        if (crc8_1(0, i) != t.t[i]) return false;
+    uint32_t a = 0, b = 0, x = 12345;  // 3-byte steps against byte steps over a pseudo-random message
+    for (int k = 0; k < 300; k++) {
+        uint32_t w = 0;
+        for (int j = 0; j < 3; j++) {
+            x = x * 1103515245u + 12345u;
+            const uint32_t by = (x >> 16) & 0xFFu;
+            a = t.t[a ^ by];
+            w = (w << 8) | by;
+        }
+        b = crc8_3(b, w);
+        if (a != b) return false;
+    }
+    return true;
+}
+static_assert(crc8_fold_matches_table(), "register CRC-8 = table CRC-8");
+
 // ----------------------------------------------------------------------------------
 // Frame header, exact zflac semantics (src/zflac.zig:343-375, 203-214, 407).
 // `err` holds errors raised before the first-frame / consistency checks; a missing
@@ -74,11 +109,10 @@ struct FrameHdr {
     bool crc_ok;
 };
 
-// `at(i)` returns header byte i (global memory, or an LDS copy in k_scan); CRC = false skips
-// the CRC-8 (the decode kernels only need the fields: candidates were filtered already).
-// `crc_tab` is the CRC-8 table (an LDS copy in k_scan: a per-lane table lookup in constant
-// memory is a global-latency load per byte).
-template <bool CRC, typename At>
+// `at(i)` returns header byte i (global memory, an LDS copy or registers). CRC: 0 skips the
+// CRC-8 (the decode kernels only need the fields: candidates were filtered already), 1 looks
+// it up in `crc_tab` (global memory, or an LDS copy), 2 computes it in registers (k_scan).
+template <int CRC, typename At>
 __device__ __forceinline__ FrameHdr parse_frame_header_t(At&& at, uint64_t avail, uint32_t si_rate,
                                                          const uint8_t* crc_tab) {
     FrameHdr h;
@@ -149,19 +183,36 @@ __device__ __forceinline__ FrameHdr parse_frame_header_t(At&& at, uint64_t avail
         h.crc_eof = true;
         return h;
     }
-    if constexpr (CRC) {
+    if constexpr (CRC == 1) {
         uint32_t crc = 0;
         for (uint32_t i = 0; i < idx; i++) crc = crc_tab[crc ^ at(i)];
+        h.crc_ok = crc == at(idx);
+    } else if constexpr (CRC == 2) {
+        uint32_t crc = 0, i = 0;  // idx <= 15: up to five 3-byte steps, then up to two bytes
+#pragma unroll
+        for (int g = 0; g < 5; g++) {
+            if (i + 3 <= idx) {
+                crc = crc8_3(crc, (at(i) << 16) | (at(i + 1) << 8) | at(i + 2));
+                i += 3;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 2; g++) {
+            if (i < idx) {
+                crc = crc8_1(crc, at(i));
+                i++;
+            }
+        }
         h.crc_ok = crc == at(idx);
     }
     return h;
 }
 
 __device__ __forceinline__ FrameHdr parse_frame_header(const uint8_t* p, uint64_t avail, uint32_t si_rate) {
-    return parse_frame_header_t<true>([p](uint32_t i) -> uint32_t { return p[i]; }, avail, si_rate, CRC8.t);
+    return parse_frame_header_t<1>([p](uint32_t i) -> uint32_t { return p[i]; }, avail, si_rate, CRC8.t);
 }
 __device__ __forceinline__ FrameHdr parse_frame_fields(const uint8_t* p, uint64_t avail, uint32_t si_rate) {
-    return parse_frame_header_t<false>([p](uint32_t i) -> uint32_t { return p[i]; }, avail, si_rate, nullptr);
+    return parse_frame_header_t<0>([p](uint32_t i) -> uint32_t { return p[i]; }, avail, si_rate, nullptr);
 }
 
 

@@ -1144,6 +1144,9 @@ void hub_flush(Md5Hub& h) {
 }
 
 void hub_flush_runs(Md5Hub& h) {
+    // fault injection for the tests only (tests/test_gpu.py: a failed hub launch must not
+    // poison the batch's next run): ZFLAC_FAULT_HUB_FLUSH=1 makes this flush throw
+    if (const char* f = std::getenv("ZFLAC_FAULT_HUB_FLUSH"); f && f[0] == '1') throw DeviceError{};
     hipStream_t hs = h.st[h.next++ % h.n_st];
     Md5Segs sg;
     std::memset(&sg, 0, sizeof(sg));
@@ -1187,6 +1190,7 @@ void hub_forget(zflac_batch* b) {
     std::lock_guard<std::mutex> lock(h.mu);
     h.pend.erase(std::remove(h.pend.begin(), h.pend.end(), b), h.pend.end());
     b->md5_pending = false;
+    b->md5_failed = false;  // a forgotten run has no hash to fail; never leak into the next run
 }
 
 // Phase 1 of a run: every class's parallel pipeline on the next of the device's run streams,
@@ -1218,6 +1222,7 @@ void submit_batch(zflac_batch* b) {
     if (b->md5_hub) {  // the hash of the streams this run certifies, in the device's md5 hub
         Md5Hub& h = md5_hub(b->device);
         std::lock_guard<std::mutex> lock(h.mu);
+        b->md5_failed = false;  // (a failure of an earlier run of this batch is that run's)
         b->md5_pending = true;
         h.pend.push_back(b);
         if (h.pend.size() >= std::min<uint32_t>(h.runs, MD5_MAX_SEGS)) hub_flush(h);
@@ -1800,15 +1805,18 @@ int zflac_hip_batch_ready(zflac_batch* b) {
     if (!b || !b->submitted) return -E_INVALID_ARGUMENT;
     hipError_t e = hipEventQuery(b->ev_done);
     if (e == hipSuccess && b->md5_hub) {
-        if (b->md5_pending) {  // decoded, hash not launched: launch it if the hub is idle
-            try {
-                Md5Hub& h = md5_hub(b->device);
-                std::lock_guard<std::mutex> lock(h.mu);
-                if (b->md5_pending && (!h.any || hipEventQuery(h.last) == hipSuccess)) hub_flush(h);
-            } catch (const DeviceError&) {
-                return -E_DEVICE;
+        try {
+            Md5Hub& h = md5_hub(b->device);
+            std::lock_guard<std::mutex> lock(h.mu);
+            if (b->md5_pending) {  // decoded, hash not launched: launch it if the hub is idle
+                if (!h.any || hipEventQuery(h.last) == hipSuccess) hub_flush(h);
+                return 0;
             }
-            return 0;
+            // the hub launch holding this run failed (possibly another thread's flush): ev_md5
+            // was never recorded for this run, so it must not be queried
+            if (b->md5_failed) return -E_DEVICE;
+        } catch (const DeviceError&) {
+            return -E_DEVICE;
         }
         e = hipEventQuery(b->ev_md5);
     }
@@ -1909,6 +1917,42 @@ extern "C" int zflac_hip_replay(zflac_batch** bs, int nb, int reps, int what, do
                 Class& C = *b->classes[0];
                 if (what == 4) {
                     enqueue_class(b, C, false, false);
+                    continue;
+                }
+                if (what >= 8) {  // the front alone: 8 k_scan, 16 k_scan + k_scan_chunks + k_compact
+                    ScanArgs sa{};
+                    sa.in = C.in.p;
+                    sa.streams = C.d_desc.p;
+                    sa.chunks = C.d_chunks.p;
+                    sa.n_chunks = (uint32_t)C.chunks.size();
+                    sa.chunk_cnt = C.chunk_cnt.p;
+                    sa.chunk_units = C.chunk_units.p;
+                    sa.chunk_slots = C.chunk_slots.p;
+                    sa.chunk_slot_units = C.chunk_slot_units.p;
+                    sa.status = C.status;
+                    sa.n_status = (uint32_t)C.members.size();
+                    sa.misc = C.misc.p;
+                    ck(launch_scan(sa, b->rs));
+                    if (what == 16) {
+                        ck(launch_scan_chunks(C.chunk_cnt.p, C.chunk_units.p, sa.n_chunks, C.chunk_off.p,
+                                              C.chunk_uoff.p, C.misc.p, b->rs));
+                        CompactArgs ca{};
+                        ca.in = C.in.p;
+                        ca.streams = C.d_desc.p;
+                        ca.chunks = C.d_chunks.p;
+                        ca.n_chunks = sa.n_chunks;
+                        ca.chunk_cnt = C.chunk_cnt.p;
+                        ca.chunk_slots = C.chunk_slots.p;
+                        ca.chunk_slot_units = C.chunk_slot_units.p;
+                        ca.chunk_off = C.chunk_off.p;
+                        ca.chunk_uoff = C.chunk_uoff.p;
+                        ca.cap = C.cap;
+                        ca.c_pos = C.c_pos.p;
+                        ca.c_stream = C.c_stream.p;
+                        ca.c_out = C.c_out.p;
+                        ca.overflow = C.misc.p + 1;
+                        ck(launch_compact(ca, b->rs));
+                    }
                     continue;
                 }
                 DecodeArgs da = decode_args(C);

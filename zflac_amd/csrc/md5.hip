@@ -426,11 +426,38 @@ hipError_t allow_md5_lds(size_t bytes) {
     return e;
 }
 
+// Waves per k_md5_coop workgroup on the current device: ZFLAC_MD5_WG_WAVES clamped to what
+// the device's per-workgroup LDS limit holds (16 KiB of tile per wave), 0 if not even one.
+uint32_t md5_wg_waves_dev() {
+    static std::atomic<uint64_t> cache[64];  // per device: 1 + waves (0 = not yet queried)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    const uint64_t c = cache[dev & 63].load(std::memory_order_acquire);
+    if (c) return (uint32_t)(c - 1);
+    int optin = 0, plain = 0;
+    if (hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess) optin = 0;
+    if (hipDeviceGetAttribute(&plain, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) plain = 0;
+    const size_t lim = (size_t)(optin > plain ? optin : plain);
+    const size_t per = 64 * 16 * sizeof(u32x4);
+    uint32_t w = (uint32_t)md5_wg_waves();
+    if ((size_t)w * per > lim) w = (uint32_t)(lim / per);
+    cache[dev & 63].store(1 + w, std::memory_order_release);
+    return w;
+}
+
 template <int MODE>
 hipError_t launch_coop(const Md5Segs& sg, uint32_t n, hipStream_t st) {
-    const uint32_t w = (uint32_t)md5_wg_waves();
+    const uint32_t w = md5_wg_waves_dev();
+    if (w == 0) {  // no room for a tile: the lane-load kernel
+        hipLaunchKernelGGL(k_md5_multi, dim3((n + 63) / 64), dim3(64), 0, st, sg);
+        return hipGetLastError();
+    }
     const size_t lds = (size_t)w * 64 * 16 * sizeof(u32x4);
-    if (const hipError_t e = allow_md5_lds<MODE>(lds); e != hipSuccess) return e;
+    if (const hipError_t e = allow_md5_lds<MODE>(lds); e != hipSuccess) {
+        (void)hipGetLastError();  // the attribute was refused: the lane-load kernel instead
+        hipLaunchKernelGGL(k_md5_multi, dim3((n + 63) / 64), dim3(64), 0, st, sg);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_md5_coop<MODE>, dim3((n + 64 * w - 1) / (64 * w)), dim3(64 * w), lds, st, sg);
     return hipGetLastError();
 }

@@ -84,19 +84,19 @@ __device__ __forceinline__ uint32_t lane_above(uint32_t v) {
 // from its window and the next one staged in the lane's own 32-byte LDS slot: no chain of
 // dependent global byte reads, which kept each workgroup alive for several memory round
 // trips.
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
-    const uint32_t chunk = blockIdx.x;
-    if (chunk >= a.n_chunks) return;
-    // the run's status words and counters start at zero (read by kernels after this one)
-    for (uint32_t i = chunk * SCAN_THREADS + threadIdx.x; i < a.n_status; i += a.n_chunks * SCAN_THREADS)
-        a.status[i] = 0;
-    if (chunk == 0 && threadIdx.x < 4) a.misc[threadIdx.x] = 0;
-    __shared__ uint32_t s_cnt;
-    __shared__ unsigned long long s_units;
-    __shared__ uint64_t s_pos[CHUNK_CAP];
-    __shared__ uint32_t s_u[CHUNK_CAP];
-    __shared__ uint8_t s_crc[256];
-    __shared__ uint4 s_hdr[SCAN_THREADS][2];  // a lane's window and the next one (candidates only)
+// LDS of one chunk's scan: the candidates found (positions sorted at the end), their count
+// and units.
+struct ScanLds {
+    uint32_t cnt;
+    unsigned long long units;
+    uint64_t pos[CHUNK_CAP];
+    uint32_t u[CHUNK_CAP];
+};
+
+
+// The candidates of chunk `chunk` into L (called by the whole workgroup; ends with a barrier,
+// the first min(cnt, CHUNK_CAP) positions sorted).
+__device__ __forceinline__ void scan_chunk(const ScanArgs& a, uint32_t chunk, ScanLds& L) {
     const ChunkDesc ch = a.chunks[chunk];
     const uint64_t abase = ch.begin & ~(uint64_t)15;
     // all of the thread's windows in flight at once (coalesced 4 KiB rows per round); the
@@ -111,10 +111,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
                                                                                  r * SCAN_THREADS * 16, ZFLAC_SCAN_AUX));
     const StreamDesc S = a.streams[ch.stream];
     if (threadIdx.x == 0) {
-        s_cnt = 0;
-        s_units = 0;
+        L.cnt = 0;
+        L.units = 0;
     }
-    s_crc[threadIdx.x & 255u] = CRC8.t[threadIdx.x & 255u];
     __syncthreads();
     const uint64_t lane_ws = abase + (uint64_t)threadIdx.x * 16;
 #pragma unroll
@@ -134,6 +133,16 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
                             (nx_mem && (v[r].w >> 24) == 0xFFu)) &&
                            ws < ch.end;
         if (__builtin_amdgcn_ballot_w64(maybe) == 0) continue;
+#if defined(ZFLAC_SCAN_ABL) && ZFLAC_SCAN_ABL == 2  // timing ablation: the existence test only
+        atomicAdd(&L.cnt, 1u);
+        continue;
+#endif
+        // the next window (the header of a sync code in this one may run into it): the next
+        // lane's registers (DPP, at this wave-uniform point), from memory only where that lane
+        // does not hold it (lane 63; a next window past the chunk end, which read as zeros).
+        // Round 5 loaded it from memory in every candidate lane: a dependent round trip in
+        // most workgroups (~3.6 frames per 32 KiB chunk of C5 data).
+        const uint4 vn = make_uint4(n0, lane_above(v[r].y), lane_above(v[r].z), lane_above(v[r].w));
         if (ws >= ch.end) continue;
         const uint32_t c0 = sync_mask(v[r].x, v[r].y), c1 = sync_mask(v[r].y, v[r].z),
                        c2 = sync_mask(v[r].z, v[r].w);
@@ -141,58 +150,91 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
         if (nx_mem && (v[r].w >> 24) == 0xFFu)
             c3 = (c3 & 0x00808080u) | ((a.in[ws + 16] & 0xFEu) == 0xF8u ? 0x80000000u : 0u);
         if ((c0 | c1 | c2 | c3) == 0 || ws >= ch.end) continue;  // no sync code: the common case
+#if defined(ZFLAC_SCAN_ABL) && ZFLAC_SCAN_ABL == 1  // timing ablation (tools/replay.py): no header parse
+        atomicAdd(&L.cnt, (uint32_t)__builtin_popcount(c0 | c1 | c2 | c3));
+        continue;
+#endif
         uint32_t cand = (c0 * 0x00204081u) >> 28 & 15u;  // bit b: a sync code at byte b
         cand |= ((c1 * 0x00204081u) >> 28 & 15u) << 4;
         cand |= ((c2 * 0x00204081u) >> 28 & 15u) << 8;
         cand |= ((c3 * 0x00204081u) >> 28 & 15u) << 12;
-        bool staged = false;
+        // the header (at most 16 bytes from p) lies in this window and the next
+        const uint4 nx = nx_mem ? *reinterpret_cast<const uint4*>(a.in + ws + 16) : vn;
         while (cand) {
             const uint32_t b = (uint32_t)__ffs(cand) - 1u;
             cand &= cand - 1u;
             const uint64_t p = ws + b;
             if (p < ch.begin || p >= ch.end) continue;
-            if (!staged) {  // the header (at most 16 bytes from p) from this window and the next
-                s_hdr[threadIdx.x][0] = v[r];
-                s_hdr[threadIdx.x][1] = *reinterpret_cast<const uint4*>(a.in + ws + 16);
-                staged = true;
-            }
-            const uint8_t* hb = reinterpret_cast<const uint8_t*>(&s_hdr[threadIdx.x][0]) + b;
-            const FrameHdr h = parse_frame_header_t<true>([hb](uint32_t i) -> uint32_t { return hb[i]; },
-                                                          S.in_end - p, S.si_rate, s_crc);
+            // header bytes b..b+15 into four registers (little-endian words): a two-stage
+            // dword shift by b >> 2, then v_alignbyte by b & 3; parsed and CRC-checked there
+            // (round 5 staged the windows in LDS and parsed byte by byte with table lookups:
+            // ~16 dependent LDS round trips per candidate, 15 of k_scan's 83 us)
+            // (named registers, no arrays: an indexed array here became scratch / LDS)
+            const bool s8 = (b & 8u) != 0, s4 = (b & 4u) != 0;
+            const uint32_t x0 = s8 ? v[r].z : v[r].x, x1 = s8 ? v[r].w : v[r].y, x2 = s8 ? nx.x : v[r].z,
+                           x3 = s8 ? nx.y : v[r].w, x4 = s8 ? nx.z : nx.x, x5 = s8 ? nx.w : nx.y;
+            const uint32_t y0 = s4 ? x1 : x0, y1 = s4 ? x2 : x1, y2 = s4 ? x3 : x2, y3 = s4 ? x4 : x3,
+                           y4 = s4 ? x5 : x4;
+            const uint32_t sb = b & 3u;
+            const uint32_t h0 = __builtin_amdgcn_alignbyte(y1, y0, sb), h1 = __builtin_amdgcn_alignbyte(y2, y1, sb),
+                           h2 = __builtin_amdgcn_alignbyte(y3, y2, sb), h3 = __builtin_amdgcn_alignbyte(y4, y3, sb);
+            const FrameHdr h = parse_frame_header_t<2>(
+                [h0, h1, h2, h3](uint32_t i) -> uint32_t {  // byte i: v_perm from 8 bytes, zeros above
+                    const uint32_t sel = (i & 7u) | 0x0C0C0C00u;
+                    return (i & 8u) ? __builtin_amdgcn_perm(h3, h2, sel) : __builtin_amdgcn_perm(h1, h0, sel);
+                },
+                S.in_end - p, S.si_rate, nullptr);
             if (!candidate_ok(h, S)) continue;
-            const uint32_t slot = atomicAdd(&s_cnt, 1u);
+            const uint32_t slot = atomicAdd(&L.cnt, 1u);
             const uint32_t units = h.bs * S.nch;
-            atomicAdd(&s_units, (unsigned long long)units);
+            atomicAdd(&L.units, (unsigned long long)units);
             if (slot < CHUNK_CAP) {
-                s_pos[slot] = p;
-                s_u[slot] = units;
+                L.pos[slot] = p;
+                L.u[slot] = units;
             }
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t n = s_cnt;
+        const uint32_t n = L.cnt;
         const uint32_t m = n < CHUNK_CAP ? n : CHUNK_CAP;
         for (uint32_t i = 1; i < m; i++) {  // insertion sort by position (m is tiny)
-            uint64_t p = s_pos[i];
-            uint32_t u = s_u[i];
+            uint64_t p = L.pos[i];
+            uint32_t u = L.u[i];
             int j = (int)i - 1;
-            while (j >= 0 && s_pos[j] > p) {
-                s_pos[j + 1] = s_pos[j];
-                s_u[j + 1] = s_u[j];
+            while (j >= 0 && L.pos[j] > p) {
+                L.pos[j + 1] = L.pos[j];
+                L.u[j + 1] = L.u[j];
                 j--;
             }
-            s_pos[j + 1] = p;
-            s_u[j + 1] = u;
+            L.pos[j + 1] = p;
+            L.u[j + 1] = u;
         }
-        a.chunk_cnt[chunk] = n;
-        a.chunk_units[chunk] = s_units;
     }
     __syncthreads();
-    const uint32_t m = s_cnt < CHUNK_CAP ? s_cnt : CHUNK_CAP;
+}
+
+// The run's status words and counters start at zero (read by kernels after this one).
+__device__ __forceinline__ void zero_run_words(const ScanArgs& a, uint32_t chunk) {
+    for (uint32_t i = chunk * SCAN_THREADS + threadIdx.x; i < a.n_status; i += a.n_chunks * SCAN_THREADS)
+        a.status[i] = 0;
+    if (chunk == 0 && threadIdx.x < 4) a.misc[threadIdx.x] = 0;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
+    const uint32_t chunk = blockIdx.x;
+    if (chunk >= a.n_chunks) return;
+    zero_run_words(a, chunk);
+    __shared__ ScanLds L;
+    scan_chunk(a, chunk, L);
+    if (threadIdx.x == 0) {
+        a.chunk_cnt[chunk] = L.cnt;
+        a.chunk_units[chunk] = L.units;
+    }
+    const uint32_t m = L.cnt < CHUNK_CAP ? L.cnt : CHUNK_CAP;
     if (threadIdx.x < m) {
-        a.chunk_slots[(uint64_t)chunk * CHUNK_CAP + threadIdx.x] = s_pos[threadIdx.x];
-        a.chunk_slot_units[(uint64_t)chunk * CHUNK_CAP + threadIdx.x] = s_u[threadIdx.x];
+        a.chunk_slots[(uint64_t)chunk * CHUNK_CAP + threadIdx.x] = L.pos[threadIdx.x];
+        a.chunk_slot_units[(uint64_t)chunk * CHUNK_CAP + threadIdx.x] = L.u[threadIdx.x];
     }
 }
 
@@ -291,12 +333,14 @@ constexpr int COMPACT_CHUNKS = SCAN_THREADS / 64;  // chunks per workgroup: one 
 
 // Overflowed chunk (more than CHUNK_CAP candidates): ordered two-pass rescan of each 4 KiB
 // sub-range with a workgroup-wide exclusive scan. Called at workgroup-uniform points.
-__device__ void compact_rescan(const CompactArgs& a, uint32_t chunk) {
-    const ChunkDesc ch = a.chunks[chunk];
-    const StreamDesc S = a.streams[ch.stream];
-    const uint32_t off = a.chunk_off[chunk];
-    const unsigned long long ubase = a.chunk_uoff[S.first_chunk];
-    const unsigned long long u0 = a.chunk_uoff[chunk];
+// `off`: the chunk's first candidate index; `urel`: units of the stream before the chunk;
+// `overflow` is set when the table is too small.
+__device__ void compact_rescan_at(const uint8_t* in, const StreamDesc* streams, const ChunkDesc* chunks, uint32_t chunk,
+                                  uint32_t off, unsigned long long urel, uint32_t cap, uint64_t* c_pos,
+                                  uint32_t* c_stream, uint64_t* c_out, uint32_t* overflow) {
+    const ChunkDesc ch = chunks[chunk];
+    const StreamDesc S = streams[ch.stream];
+    auto parse = [&](uint64_t, uint64_t p) -> FrameHdr { return parse_frame_header(in + p, S.in_end - p, S.si_rate); };
     __shared__ uint32_t s_c[SCAN_THREADS];
     __shared__ unsigned long long s_u[SCAN_THREADS];
     __shared__ uint32_t s_base_c;
@@ -313,8 +357,8 @@ __device__ void compact_rescan(const CompactArgs& a, uint32_t chunk) {
         uint32_t c = 0;
         unsigned long long u = 0;
         if (ws < ch.end) {
-            scan_window(a.in, ws, ch.begin, ch.end, [&](uint64_t p) {
-                const FrameHdr h = parse_frame_header(a.in + p, S.in_end - p, S.si_rate);
+            scan_window(in, ws, ch.begin, ch.end, [&](uint64_t p) {
+                const FrameHdr h = parse(ws, p);
                 if (!candidate_ok(h, S)) return;
                 c++;
                 u += h.bs * S.nch;
@@ -338,16 +382,16 @@ __device__ void compact_rescan(const CompactArgs& a, uint32_t chunk) {
         uint32_t rc = s_base_c + s_c[threadIdx.x] - c;
         unsigned long long ru = s_base_u + s_u[threadIdx.x] - u;
         if (ws < ch.end && c) {
-            scan_window(a.in, ws, ch.begin, ch.end, [&](uint64_t p) {
-                const FrameHdr h = parse_frame_header(a.in + p, S.in_end - p, S.si_rate);
+            scan_window(in, ws, ch.begin, ch.end, [&](uint64_t p) {
+                const FrameHdr h = parse(ws, p);
                 if (!candidate_ok(h, S)) return;
                 const uint32_t idx = off + rc;
-                if (idx < a.cap) {
-                    a.c_pos[idx] = p;
-                    a.c_stream[idx] = ch.stream;
-                    a.c_out[idx] = S.out_base + (u0 - ubase + ru);
-                } else {
-                    atomicOr(a.overflow, 1u);
+                if (idx < cap) {
+                    c_pos[idx] = p;
+                    c_stream[idx] = ch.stream;
+                    c_out[idx] = S.out_base + (urel + ru);
+                } else if (overflow) {
+                    atomicOr(overflow, 1u);
                 }
                 rc++;
                 ru += h.bs * S.nch;
@@ -393,7 +437,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_compact(CompactArgs a) {
 #pragma unroll 1
     for (uint32_t j = 0; j < (uint32_t)COMPACT_CHUNKS; j++) {  // workgroup-uniform
         const uint32_t cj = c0 + j;
-        if (cj < a.n_chunks && a.chunk_cnt[cj] > CHUNK_CAP) compact_rescan(a, cj);
+        if (cj < a.n_chunks && a.chunk_cnt[cj] > CHUNK_CAP) {
+            const StreamDesc& S = a.streams[a.chunks[cj].stream];
+            compact_rescan_at(a.in, a.streams, a.chunks, cj, a.chunk_off[cj],
+                              a.chunk_uoff[cj] - a.chunk_uoff[S.first_chunk], a.cap, a.c_pos, a.c_stream, a.c_out,
+                              a.overflow);
+        }
     }
 }
 

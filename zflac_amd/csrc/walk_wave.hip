@@ -316,7 +316,7 @@ __global__ __launch_bounds__(WW_THREADS) void k_walk_wave(DecodeArgs a) {
         W.init(0);
         // the frame header from the window (its at most 16 + 16 bytes are words 0..7)
         const uint32_t hb = (uint32_t)(pos & 15);
-        const FrameHdr h = parse_frame_header_t<false>([&](uint32_t i) -> uint32_t { return W.byte(hb + i); },
+        const FrameHdr h = parse_frame_header_t<0>([&](uint32_t i) -> uint32_t { return W.byte(hb + i); },
                                                        S.in_end > pos ? S.in_end - pos : 0, S.si_rate, nullptr);
         const int bps = depth_bits(h.dcode, S.si_bps);
         // the frame decodes only with these (setup_frame in decode.inc)
