@@ -116,6 +116,10 @@ def parse_args():
     ap.add_argument("--md5-runs", type=int, default=8, help="decode+MD5 leg: runs per md5 hub launch (ZFLAC_MD5_RUNS)")
     ap.add_argument("--md5-hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES of the decode+MD5 leg's process (default: run + hub streams)")
+    ap.add_argument("--timed-events", choices=["on", "off"], default="off",
+                    help="HIP timing events (5 per run) in the timed steps too (on: stages_ms_overlapped); "
+                         "the serial leg always records them. Off by default since round 6: same box, "
+                         "alternating, 700-710k vs 673-695k Msamples/s with them on (profiles/r6_events_ab.json)")
     ap.add_argument("--sched", choices=["rr", "ready"], default="rr",
                     help="headline runs in flight: round robin, or whichever batch finished first")
     ap.add_argument("--md5-leg-child", action="store_true", help=argparse.SUPPRESS)
@@ -529,7 +533,10 @@ def main():
     # waited for, so one run's scan and walk execute beside the other's decode. Every step
     # still decodes and verifies the whole shard.
     n_inf = max(1, min(args.inflight, args.steps))  # every batch runs (and is verified)
-    batches = [zflac_amd.Batch(streams, device=device, timing=True) for _ in range(n_inf)]
+    timed_ev = args.timed_events == "on" or n_inf == 1  # (one in flight: no serial leg, the timed runs give the times)
+    batches = [zflac_amd.Batch(streams, device=device, timing=timed_ev) for _ in range(n_inf)]
+    # the serial leg's batch always records its stage events (the isolated kernel times)
+    serial_batch = batches[:1] if timed_ev else [zflac_amd.Batch(streams, device=device, timing=True)]
     STAGES = ("scan_ms", "walk_ms", "decode_ms", "verify_ms")
 
     def run_steps(k, bs, rec=None):
@@ -576,20 +583,20 @@ def main():
     rec = None
     if n_inf > 1:
         half = args.steps // 2
-        run_steps(half, batches[:1])
+        run_steps(half, serial_batch)
         rec = {n: [] for n in STAGES}
         t1 = time.perf_counter()
-        run_steps(args.steps - half, batches[:1], rec)
+        run_steps(args.steps - half, serial_batch, rec)
         serial = (time.perf_counter() - t1) / (args.steps - half)
     run_steps(args.warmup, batches)
     progress("warm-up done")
     barrier_sync()
     t0 = time.perf_counter()
     rec_ov = {n: [] for n in STAGES}
-    run_steps(args.steps, batches, rec_ov)
+    run_steps(args.steps, batches, rec_ov if timed_ev else None)
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    tm = batches[0].timings()
+    tm = batches[0].timings() or serial_batch[0].timings()
     samples_rank = tm.samples
     in_bytes, out_bytes = tm.input_bytes, tm.output_bytes
     if rec is None:
@@ -603,6 +610,8 @@ def main():
         errs, n_compared = verify(batches, streams)
     for b in batches[1:]:
         b.close()
+    if serial_batch[0] is not batches[0]:
+        serial_batch[0].close()
     batch = batches[0]
     tot = aggregate(dist, coll_dev, elapsed, samples_rank, in_bytes, out_bytes, len(errs))
     elapsed = tot.elapsed_s
@@ -679,7 +688,8 @@ def main():
                           "verify": round(float(np.mean(ver_ms)), 4)},
             "stages_ms_overlapped": {"scan+compact": round(float(np.mean(rec_ov["scan_ms"])), 4),
                                      "walk": round(float(np.mean(rec_ov["walk_ms"])), 4),
-                                     "decode": round(float(np.mean(rec_ov["decode_ms"])), 4)} if serial else None,
+                                     "decode": round(float(np.mean(rec_ov["decode_ms"])), 4)}
+            if serial and rec_ov["decode_ms"] else None,
             "traffic_detail": pmc,
             "lib_sha256": lib_sha[:16],
             "build_id": bid,

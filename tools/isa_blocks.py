@@ -38,7 +38,7 @@ def classify(op):
 
 def blocks(lines):
     out = []
-    cur = {"name": "entry", "ins": [], "succ": []}
+    cur = {"name": "entry", "ins": [], "succ": [], "loop": None}
     for l in lines:
         s = l.split(";")[0].rstrip()
         m = re.match(r"^(\.LBB\S+):", s)
@@ -51,8 +51,15 @@ def blocks(lines):
             if cur["ins"] and not cur["ins"][-1].startswith(("s_branch", "s_setpc", "s_endpgm")):
                 cur["succ"].append(m.group(1))
             out.append(cur)
-            cur = {"name": m.group(1), "ins": [], "succ": []}
+            cur = {"name": m.group(1), "ins": [], "succ": [], "loop": None}
+            lm = re.search(r"(?:Header=|Loop: Header=)BB\d+_(\d+) Depth=(\d+)", l)
+            hm = re.search(r"This Loop Header: Depth=(\d+)", l)
+            if lm:
+                cur["loop"] = (int(lm.group(1)), int(lm.group(2)))
+            pending_header = hm is not None
             continue
+        if l.strip().startswith("; =>  This Loop Header: Depth=") and cur["loop"] is None:
+            cur["loop"] = (int(cur["name"].split(".")[-1]), int(l.strip().split("=")[-1]))
         s = s.strip()
         if not s or s.startswith(".") or s.endswith(":"):
             continue
@@ -81,8 +88,10 @@ def main():
         b["c"] = c
         if show and b["name"] == show:
             print("\n".join(b["ins"]))
+        rl = sum(1 for i in b["ins"] if i.startswith("v_readlane"))
         if not show and c.get("valu", 0) >= minv:
-            print(f"{b['name']:>14} n={len(b['ins']):5d} valu={c.get('valu', 0):4d} salu={c.get('salu', 0):3d} "
+            lp = f"L{b['loop'][0]}/{b['loop'][1]}" if b.get("loop") else "-"
+            print(f"{b['name']:>14} {lp:>9} n={len(b['ins']):5d} valu={c.get('valu', 0):4d} rl={rl:2d} salu={c.get('salu', 0):3d} "
                   f"lds={c.get('lds', 0):3d} vmem={c.get('vmem', 0):3d} wait={c.get('wait', 0):3d} -> {' '.join(b['succ'])}")
     if not show:
         print("total", tot, "blocks", len(bl))
