@@ -111,9 +111,13 @@ def parse_args():
                          "profiles/r5_md5_steps_sweep.json)")
     ap.add_argument("--md5-run-streams", type=int, default=5,
                     help="decode+MD5 leg: the library's run streams (ZFLAC_RUN_STREAMS)")
-    ap.add_argument("--md5-hub-streams", type=int, default=2,
+    ap.add_argument("--md5-hub-streams", type=int, default=3,
                     help="decode+MD5 leg: md5 hub streams (ZFLAC_HUB_STREAMS), each launch hashing --md5-runs runs")
     ap.add_argument("--md5-runs", type=int, default=8, help="decode+MD5 leg: runs per md5 hub launch (ZFLAC_MD5_RUNS)")
+    # (64 of 256 CUs with three hub streams: 467-474k vs 435-463k shared, two same-box sweeps,
+    # profiles/r6_md5_hub_cus.json)
+    ap.add_argument("--md5-hub-cus", type=int, default=64,
+                    help="decode+MD5 leg: CUs of the md5 hub's own (ZFLAC_HUB_CUS; 0 = hub and runs share every CU)")
     ap.add_argument("--md5-hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES of the decode+MD5 leg's process (default: run + hub streams)")
     ap.add_argument("--timed-events", choices=["on", "off"], default="off",
@@ -351,7 +355,7 @@ def md5_leg(args, streams, device: int, barrier=lambda: None):
     stream, ~7-9 ms for this shard) while other batches' runs decode on the run streams.
     `md5_inflight` batches in completion order (run_ready_order), `md5_steps` timed runs."""
     for k, v in (("ZFLAC_RUN_STREAMS", args.md5_run_streams), ("ZFLAC_HUB_STREAMS", args.md5_hub_streams),
-                 ("ZFLAC_MD5_RUNS", args.md5_runs)):
+                 ("ZFLAC_MD5_RUNS", args.md5_runs), ("ZFLAC_HUB_CUS", args.md5_hub_cus)):
         os.environ.setdefault(k, str(v))  # read by the library when it creates the device's streams
     import zflac_amd
 
@@ -378,7 +382,7 @@ def md5_leg(args, streams, device: int, barrier=lambda: None):
     return {"kernel": "k_md5_coop", "md5_ms": round(float(np.mean(rec)), 4), "all_match": ok, "inflight": k_md5,
             "steps": n_steps, "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             "run_streams": os.environ.get("ZFLAC_RUN_STREAMS"), "hub_streams": os.environ.get("ZFLAC_HUB_STREAMS"),
-            "runs_per_hub_launch": os.environ.get("ZFLAC_MD5_RUNS"),
+            "runs_per_hub_launch": os.environ.get("ZFLAC_MD5_RUNS"), "hub_cus": os.environ.get("ZFLAC_HUB_CUS"),
             "decode_plus_md5_msps_rank0": round(samples * n_steps / el / 1e6, 1),
             "ms_per_step": round(el / n_steps * 1e3, 4),
             "hashed_bytes_rank0": int(out_bytes),
@@ -395,14 +399,16 @@ def start_md5_child(args):
     cmd = [sys.executable, os.path.abspath(__file__), "--md5-leg-child", "--steps", str(args.steps), "--warmup",
            str(args.warmup), "--streams-per-gpu", str(args.streams_per_gpu), "--md5-inflight", str(args.md5_inflight),
            "--md5-steps", str(args.md5_steps), "--md5-run-streams", str(args.md5_run_streams),
-           "--md5-hub-streams", str(args.md5_hub_streams), "--md5-runs", str(args.md5_runs)]
+           "--md5-hub-streams", str(args.md5_hub_streams), "--md5-runs", str(args.md5_runs),
+           "--md5-hub-cus", str(args.md5_hub_cus)]
     if args.same_device:
         cmd.append("--same-device")
     if args.dry_run:
         cmd.append("--dry-run")
     q = args.md5_hw_queues or args.md5_run_streams + args.md5_hub_streams  # one hardware queue per stream
     env = dict(os.environ, GPU_MAX_HW_QUEUES=str(q), ZFLAC_RUN_STREAMS=str(args.md5_run_streams),
-               ZFLAC_HUB_STREAMS=str(args.md5_hub_streams), ZFLAC_MD5_RUNS=str(args.md5_runs))
+               ZFLAC_HUB_STREAMS=str(args.md5_hub_streams), ZFLAC_MD5_RUNS=str(args.md5_runs),
+               ZFLAC_HUB_CUS=str(args.md5_hub_cus))
     return subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE)
 
 

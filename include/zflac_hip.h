@@ -93,7 +93,10 @@ typedef struct zflac_timings {
      * history bucket the batch's launch plan had not predicted; the bucket is then added to
      * the plan, so a later run of the same batch has none */
     uint32_t rest_launches;
-    uint32_t reserved0;
+    /* (ABI 5) streams of the last run finished by the sequential chain planner (the chain
+     * check did not certify them: false syncs, a broken frame, a wrong STREAMINFO, a total
+     * unknown without a minimum frame size); 0 when the parallel pass certified every one */
+    uint32_t sequential_streams;
 } zflac_timings;
 
 typedef struct zflac_batch zflac_batch;
@@ -203,8 +206,10 @@ const char *zflac_hip_version(void);
 const char *zflac_hip_build_id(void);
 /* ABI revision of this header; bumped whenever a struct or a signature changes.
  * 3: zflac_hip_batch_timings_ex, zflac_hip_abi_version; device MD5 pipelined into submit.
- * 4: zflac_timings.rest_launches; zflac_hip_build_id; zflac_hip_batch_ready. */
-#define ZFLAC_HIP_ABI_VERSION 4
+ * 4: zflac_timings.rest_launches; zflac_hip_build_id; zflac_hip_batch_ready.
+ * 5: zflac_timings.sequential_streams (was reserved0); total-unknown streams certified by the
+ *    parallel pass. */
+#define ZFLAC_HIP_ABI_VERSION 5
 int zflac_hip_abi_version(void);
 
 #ifdef __cplusplus

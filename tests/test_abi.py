@@ -74,13 +74,14 @@ def test_kernels_compiled_for_gfx950():
 
 
 def test_abi_version_and_timings_struct():
-    """ABI revision 4; zflac_hip_batch_timings_ex takes the caller's struct size, and the
+    """ABI revision 5; zflac_hip_batch_timings_ex takes the caller's struct size, and the
     legacy entry point writes only the first-version layout (scan_ms .. md5_ms)."""
     L = _lib.load()
-    assert L.zflac_hip_abi_version() == 4
+    assert L.zflac_hip_abi_version() == 5
     t = _lib.zflac_timings()
     assert ctypes.sizeof(t) == 136
     assert _lib.zflac_timings.rest_launches.offset == 128
+    assert _lib.zflac_timings.sequential_streams.offset == 132
     assert _lib.zflac_timings.plan_ms.offset == 80  # ZFLAC_TIMINGS_V1_SIZE
     assert L.zflac_hip_batch_timings_ex(None, ctypes.byref(t), ctypes.sizeof(t)) == 14
     assert L.zflac_hip_batch_timings(None, ctypes.byref(t)) == 14

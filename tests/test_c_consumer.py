@@ -40,7 +40,7 @@ def test_builds_with_werror_and_names_match(consumer):
     """Compiles warning-free as C11 (static_asserts included) and the shim's error switch
     names every ZFLAC_E_* code as the library does."""
     r = _run(consumer, "names")
-    assert r == {"names": True, "abi": 4}
+    assert r == {"names": True, "abi": 5}
 
 
 def test_zig_shim_is_the_mirrored_switch():

@@ -387,6 +387,48 @@ def test_bucket_misprediction_still_decodes(gpu_ready):
     b.close()
 
 
+def _with_min_frame(flac: bytes, v: int) -> bytes:
+    """STREAMINFO's minimum frame size (24 bits at block offset 4) set to `v` bytes."""
+    d = bytearray(flac)
+    assert d[:4] == b"fLaC" and (d[4] & 0x7F) == 0
+    d[12:15] = v.to_bytes(3, "big")
+    return bytes(d)
+
+
+def test_unknown_total_certified_by_parallel_pass(gpu_ready):
+    """STREAMINFO total 0 (unknown): zflac reads frames until fewer than 4 bytes are left
+    (src/zflac.zig:343-350) and grows its buffer as it goes. The parallel pass reserves room by
+    STREAMINFO's minimum frame size and maximum block size and k_verify certifies the chain to
+    the end of the stream, so no stream goes to the sequential planner. A minimum frame size
+    that is too large (room for two frames) or absent, 4 trailing bytes (a frame header zflac
+    reads and rejects) and a false sync send the stream to the planner: same samples / error
+    as the oracle either way."""
+    st = synth.generate(**dict(PARITY_CONFIGS["c3_ms16_lpc8"], write_total=0, seed=4400))
+    avail = len(st.flac) - st.frames_begin
+    cases = {  # name: (stream, streams the planner finishes of the 3 in the batch)
+        "min_frame_ok": (st.flac, 0),
+        "trailing_3_bytes": (st.flac + b"\x00\x01\x02", 0),
+        "min_frame_too_large": (_with_min_frame(st.flac, avail // 2), 3),
+        "min_frame_unknown": (_with_min_frame(st.flac, 0), 3),
+        "trailing_4_bytes": (st.flac + b"\x00\x01\x02\x03", 3),
+    }
+    for name, (data, seq) in cases.items():
+        r = oracle.decode(data)
+        b = zflac_amd.Batch([data] * 3, timing=True)
+        for _ in range(2):  # the second run reuses the reservation and the unit read-back
+            b.run()
+            assert b.timings().sequential_streams == seq, name
+            for i in range(3):
+                assert b.error_name(i) == r.error, name
+                if r.error == "OK":
+                    d = b.read(i)
+                    np.testing.assert_array_equal(d.samples.values, r.samples, err_msg=name)
+                    assert d.samples.values.size == r.samples.size, name
+        b.close()
+    assert oracle.decode(st.flac).error == "OK"
+    assert oracle.decode(st.flac + b"\x00\x01\x02\x03").error != "OK"
+
+
 def test_pipelined_device_md5_overlapped(gpu_ready):
     """ZFLAC_FLAG_DEVICE_MD5 with three batches in flight (submit / wait): the certified
     streams' digests come from the k_md5 enqueued by submit, the sequential ones (a false

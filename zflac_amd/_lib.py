@@ -30,7 +30,7 @@ class zflac_timings(ctypes.Structure):
                 ("output_bytes", ctypes.c_uint64), ("samples", ctypes.c_uint64), ("walk_ms", ctypes.c_double),
                 ("md5_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("upload_ms", ctypes.c_double),
                 ("run_wall_ms", ctypes.c_double), ("read_ms", ctypes.c_double), ("host_md5_ms", ctypes.c_double),
-                ("crc16_ms", ctypes.c_double), ("rest_launches", ctypes.c_uint32), ("reserved0", ctypes.c_uint32)]
+                ("crc16_ms", ctypes.c_double), ("rest_launches", ctypes.c_uint32), ("sequential_streams", ctypes.c_uint32)]
 
 
 # every symbol include/zflac_hip.h declares, with (restype, argtypes)

@@ -206,6 +206,8 @@ struct VerifyArgs {
     const uint32_t* c_info;
     const uint32_t* c_rate;
     uint32_t* status;           // per stream: nonzero => take the sequential path
+    uint64_t* units;            // per stream, STREAMINFO total unknown: the chain's output elements
+                                // (written by its last frame; nullptr when every total is known)
 };
 
 // k_sync_list (scan.hip): sync codes in [lo, hi) with a parseable header matching the

@@ -133,6 +133,7 @@ struct ByteReader {
 
 struct StreamInfoH {
     uint16_t min_block = 0, max_block = 0;
+    uint32_t min_frame = 0;  // bytes (0: unknown)
     uint32_t sample_rate = 0;
     uint32_t channels = 0;  // count
     uint32_t bps = 0;       // bits
@@ -158,6 +159,7 @@ int parse_metadata(const uint8_t* d, size_t n, StreamInfoH& si, size_t& frames_b
             const uint8_t* p = d + r.pos;
             si.min_block = (uint16_t)((p[0] << 8) | p[1]);
             si.max_block = (uint16_t)((p[2] << 8) | p[3]);
+            si.min_frame = ((uint32_t)p[4] << 16) | ((uint32_t)p[5] << 8) | p[6];
             si.sample_rate = ((uint32_t)p[10] << 12) | ((uint32_t)p[11] << 4) | (p[12] >> 4);
             si.channels = ((p[12] >> 1) & 7) + 1;
             si.bps = (((p[12] & 1) << 4) | (p[13] >> 4)) + 1;
@@ -337,6 +339,11 @@ struct Class {
     } pin;
     uint32_t* h_misc = nullptr;
     uint32_t* h_status = nullptr;
+    // members whose STREAMINFO total is unknown but whose output is reserved (unknown_total_cap):
+    // k_verify certifies their chain to the end of the stream and writes its length here
+    bool any_unknown = false;
+    DevBuf<uint64_t> units;
+    uint64_t* h_units = nullptr;  // pinned mirror, after the status words
 };
 
 }  // namespace
@@ -562,6 +569,22 @@ uint32_t plan_buckets(const zflac_batch* b, const Class& C, const zflac_stream* 
     return mask;
 }
 
+// Output room for a stream whose STREAMINFO total is 0 (unknown): zflac then reads frames until
+// fewer than 4 bytes are left (src/zflac.zig:343-350) and grows its buffer as it goes. The fast
+// path reserves room for every frame the stream can hold by STREAMINFO's minimum frame size and
+// maximum block size; a chain that does not fit it (STREAMINFO wrong) is not certified
+// (k_verify) and goes to the sequential planner, as does a stream without a minimum frame
+// size. 0 = no reservation.
+uint64_t unknown_total_cap(const StreamState& s) {
+    if (!s.si.min_frame) return 0;
+    const uint64_t avail = s.len - s.frames_begin;
+    const uint64_t frames = avail / s.si.min_frame + 1;
+    const uint64_t cap = frames * (s.si.max_block ? s.si.max_block : 65535u) * (uint64_t)s.nch;
+    // (a memory bound: at most 32 output elements per input byte, ~2x the least compressed
+    // 16-bit stereo stream (verbatim) would need)
+    return cap <= 32 * avail + (1u << 20) ? cap : 0;
+}
+
 void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     C.full_mask = plan_buckets(b, C, src);
     const int esz = esz_of_kind(C.kind);
@@ -593,7 +616,8 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
         D.out_base = out;
         D.valid_total = s.si.total > 0;
         D.total = D.valid_total ? s.si.total * (uint64_t)s.nch : 0;
-        D.out_cap = D.total;
+        D.out_cap = D.valid_total ? D.total : unknown_total_cap(s);
+        if (!D.valid_total && D.out_cap) C.any_unknown = true;
         out += D.out_cap;
         D.rate_hz = s.first.rate;
         D.si_rate = s.si.sample_rate;
@@ -615,7 +639,9 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
         D.end_chunk = (uint32_t)C.chunks.size();
         const uint64_t minb = std::max<uint64_t>(16, s.si.min_block ? s.si.min_block : 16);
         // (at most one candidate per two bytes: a huge STREAMINFO total cannot inflate it)
-        const uint64_t est = std::min<uint64_t>(s.si.total ? s.si.total / minb : s.len / 16, s.len / 2) + 2;
+        const uint64_t est =
+            std::min<uint64_t>(s.si.total ? s.si.total / minb : (s.si.min_frame ? s.len / s.si.min_frame : s.len / 16),
+                               s.len / 2) + 2;
         est_frames += est;
         // fixed blocking with a known total: zflac reads exactly ceil(total / block) frames (:341)
         const bool fixed = s.si.min_block == s.si.max_block && s.si.min_block >= 16;
@@ -645,11 +671,16 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     C.misc.alloc(4 + C.members.size());
     C.status = C.misc.p + 4;
     C.dummy.alloc(DUMMY_BYTES + PROBE_BYTES);
-    ck(hipHostMalloc(reinterpret_cast<void**>(&C.pin.p), (4 + C.members.size()) * sizeof(uint32_t),
-                     hipHostMallocDefault));
-    std::memset(C.pin.p, 0, (4 + C.members.size()) * sizeof(uint32_t));
+    const size_t units_at = (4 + C.members.size() + 1) & ~(size_t)1;  // (u32 index, 8-byte aligned)
+    const size_t pin_words = units_at + (C.any_unknown ? 2 * C.members.size() : 0);
+    ck(hipHostMalloc(reinterpret_cast<void**>(&C.pin.p), pin_words * sizeof(uint32_t), hipHostMallocDefault));
+    std::memset(C.pin.p, 0, pin_words * sizeof(uint32_t));
     C.h_misc = C.pin.p;
     C.h_status = C.pin.p + 4;
+    if (C.any_unknown) {
+        C.units.alloc(C.members.size());
+        C.h_units = reinterpret_cast<uint64_t*>(C.pin.p + units_at);
+    }
     C.cap = (uint32_t)std::min<uint64_t>(est_frames + C.chunks.size() * 2 + 1024, 0x7FFFFFFFull);
     C.est_frames = est_frames;
     C.grid_frames = (uint32_t)std::min<uint64_t>(grid_frames + grid_frames / 64 + 64, C.cap);
@@ -750,10 +781,13 @@ void enqueue_class(zflac_batch* b, Class& C, bool timing_first, bool timing_last
     va.c_info = C.c_info.p;
     va.c_rate = C.c_rate.p;
     va.status = C.status;
+    va.units = C.any_unknown ? C.units.p : nullptr;
     ck(launch_verify(va, C.cap, st));
     if (timing_last) ck(hipEventRecord(b->ev[3], st));
     // the counters and the status words in one read-back (contiguous on both sides)
     ck(hipMemcpyAsync(C.h_misc, C.misc.p, (4 + C.members.size()) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    if (C.any_unknown)
+        ck(hipMemcpyAsync(C.h_units, C.units.p, C.members.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
 }
 
 // After a run whose order-8 launch found frame groups of a bucket the host did not
@@ -780,8 +814,11 @@ void enqueue_rest(zflac_batch* b, Class& C) {
     va.c_info = C.c_info.p;
     va.c_rate = C.c_rate.p;
     va.status = C.status;
+    va.units = C.any_unknown ? C.units.p : nullptr;
     ck(launch_verify(va, C.cap, st));
     ck(hipMemcpyAsync(C.h_status, C.status, C.members.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    if (C.any_unknown)
+        ck(hipMemcpyAsync(C.h_units, C.units.p, C.members.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ck(hipStreamSynchronize(st));
 }
 
@@ -1093,11 +1130,32 @@ struct DeviceScope {
     }
 };
 
+// ZFLAC_HUB_CUS=N (N > 0): the md5 hub's streams on N CUs of their own and the run streams on
+// the others (hipExtStreamCreateWithCUMask; the lowest N bits of the device's CU mask). The
+// hash is one serial chain per stream, compute-only: on CUs it shares with the decode, its
+// waves slow the decode waves there, and a decode launch ends with its slowest wave.
+static uint32_t hub_cus() {
+    const char* e = std::getenv("ZFLAC_HUB_CUS");
+    return e ? (uint32_t)std::max(0, atoi(e)) : 0u;
+}
+
 DeviceStreams::DeviceStreams() : hub_p(new Md5Hub()), hub(*hub_p) {
     if (const char* e = std::getenv("ZFLAC_RUN_STREAMS")) n_run = (uint32_t)std::max(1, std::min(atoi(e), MAX_RUN_STREAMS));
     if (const char* e = std::getenv("ZFLAC_HUB_STREAMS")) hub.n_st = (uint32_t)std::max(1, std::min(atoi(e), MAX_HUB_STREAMS));
-    for (uint32_t i = 0; i < n_run; i++) ck(hipStreamCreateWithFlags(&run[i], hipStreamNonBlocking));
-    for (uint32_t i = 0; i < hub.n_st; i++) ck(hipStreamCreateWithFlags(&hub.st[i], hipStreamNonBlocking));
+    const uint32_t nh = hub_cus();
+    int dev = 0, ncu = 0;
+    ck(hipGetDevice(&dev));
+    ck(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    if (nh > 0 && nh < (uint32_t)ncu) {
+        const uint32_t words = ((uint32_t)ncu + 31) / 32;
+        std::vector<uint32_t> hm(words, 0u), rm(words, 0u);
+        for (uint32_t c = 0; c < (uint32_t)ncu; c++) (c < nh ? hm : rm)[c / 32] |= 1u << (c % 32);
+        for (uint32_t i = 0; i < n_run; i++) ck(hipExtStreamCreateWithCUMask(&run[i], words, rm.data()));
+        for (uint32_t i = 0; i < hub.n_st; i++) ck(hipExtStreamCreateWithCUMask(&hub.st[i], words, hm.data()));
+    } else {
+        for (uint32_t i = 0; i < n_run; i++) ck(hipStreamCreateWithFlags(&run[i], hipStreamNonBlocking));
+        for (uint32_t i = 0; i < hub.n_st; i++) ck(hipStreamCreateWithFlags(&hub.st[i], hipStreamNonBlocking));
+    }
     ck(hipEventCreateWithFlags(&hub.last, hipEventDisableTiming));
     if (const char* e = std::getenv("ZFLAC_MD5_RUNS")) hub.runs = (uint32_t)std::max(1, std::min(atoi(e), MD5_MAX_SEGS));
 }
@@ -1245,7 +1303,7 @@ void finish_batch(zflac_batch* b) {
         }
         ck(hipEventSynchronize(b->ev_md5));
     }
-    uint32_t rest_launches = 0;
+    uint32_t rest_launches = 0, sequential = 0;
     for (size_t ci = 0; ci < b->classes.size(); ci++) {
         Class& C = *b->classes[ci];
         for (int attempt = 0; attempt < 3; attempt++) {
@@ -1333,7 +1391,7 @@ void finish_batch(zflac_batch* b) {
                 const StreamDesc& D = C.desc[m];
                 s.err = 0;
                 s.dev_samples = C.out.p + D.out_base * esz;
-                s.info.n_samples = D.total;
+                s.info.n_samples = D.valid_total ? D.total : C.h_units[m];
                 s.info.channels = (uint8_t)s.nch;
                 s.info.sample_rate = s.first.rate;
                 s.info.bits_per_sample = (uint8_t)depth_bits_h(s.first.dcode, (int)s.si.bps);
@@ -1358,6 +1416,7 @@ void finish_batch(zflac_batch* b) {
                     ck(hipMemcpy(h_off.data(), C.chunk_off.p, h_off.size() * 4, hipMemcpyDeviceToHost));
                 }
                 finish_stream_sequential(b, C, (uint32_t)m, h_off, std::min(C.h_misc[0], C.cap));
+                sequential++;
             }
             s.info.samples_bytes = s.info.n_samples * esz;
             if (!s.err) {
@@ -1377,6 +1436,7 @@ void finish_batch(zflac_batch* b) {
     b->timings.output_bytes = out_bytes;
     b->timings.samples = samples;
     b->timings.rest_launches = rest_launches;
+    b->timings.sequential_streams = sequential;
 }
 
 // MD5 of the decoded stream exactly as zflac hashes it: before left-justify, 24-bit

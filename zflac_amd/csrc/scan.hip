@@ -456,7 +456,9 @@ __global__ void k_verify(VerifyArgs a) {
     if (t < a.n_streams) {
         const StreamDesc S = a.streams[t];
         const uint32_t f0 = a.chunk_off[S.first_chunk], f1 = a.chunk_off[S.end_chunk];
-        if (f1 <= f0 || f1 > nframes || !S.valid_total || a.c_pos[f0] != S.in_begin) atomicOr(&a.status[t], 1u);
+        // (total unknown: certified only with room reserved for it, see alloc_class)
+        if (f1 <= f0 || f1 > nframes || (!S.valid_total && !a.units) || a.c_pos[f0] != S.in_begin)
+            atomicOr(&a.status[t], 1u);
     }
     if (t >= nframes) return;
     const uint32_t s = a.c_stream[t];
@@ -472,8 +474,18 @@ __global__ void k_verify(VerifyArgs a) {
     const uint64_t units = (uint64_t)bs * S.nch;
     if (bs == 1 && rel + S.nch < S.total) bad = true;  // :405
     const uint64_t end_rel = rel + units;
-    if (end_rel > S.total || end_rel > S.out_cap) bad = true;     // zflac would grow the buffer
-    if (end_rel < S.total && (t + 1 >= f1 || a.c_pos[t + 1] != a.c_end[t])) bad = true;
+    if (end_rel > S.out_cap) bad = true;
+    if (S.valid_total) {
+        if (end_rel > S.total) bad = true;  // zflac would grow the buffer and read on to EOF
+        if (end_rel < S.total && (t + 1 >= f1 || a.c_pos[t + 1] != a.c_end[t])) bad = true;
+    } else {
+        // total unknown: frames until fewer than 4 bytes are left (:343-350 EndOfStream
+        // break); the frame that ends there is the chain's last and holds its length
+        const bool last = a.c_end[t] + 4 > S.in_end;
+        if (!last && (t + 1 >= f1 || a.c_pos[t + 1] != a.c_end[t])) bad = true;
+        if (last && t + 1 < f1) bad = true;  // a candidate in the last bytes: the planner decides
+        if (last && a.units) a.units[s] = end_rel;
+    }
     if (bad) atomicOr(&a.status[s], 1u);
 }
 
