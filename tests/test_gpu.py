@@ -397,20 +397,23 @@ def _with_min_frame(flac: bytes, v: int) -> bytes:
 
 def test_unknown_total_certified_by_parallel_pass(gpu_ready):
     """STREAMINFO total 0 (unknown): zflac reads frames until fewer than 4 bytes are left
-    (src/zflac.zig:343-350) and grows its buffer as it goes. The parallel pass reserves room by
-    STREAMINFO's minimum frame size and maximum block size and k_verify certifies the chain to
-    the end of the stream, so no stream goes to the sequential planner. A minimum frame size
-    that is too large (room for two frames) or absent, 4 trailing bytes (a frame header zflac
-    reads and rejects) and a false sync send the stream to the planner: same samples / error
-    as the oracle either way."""
+    (src/zflac.zig:343-350) and grows its buffer as it goes. The batch's creation scans the
+    stream once and reserves the units its sync candidates claim; k_verify then certifies the
+    chain to the end of the stream, so no stream goes to the sequential planner, whatever
+    STREAMINFO's frame sizes say. 4 trailing bytes (a frame header zflac reads and rejects) and
+    planted false syncs send the stream to the planner: same samples / error as the oracle
+    either way."""
     st = synth.generate(**dict(PARITY_CONFIGS["c3_ms16_lpc8"], write_total=0, seed=4400))
     avail = len(st.flac) - st.frames_begin
+    planted = synth.generate(channels=2, bps=16, stereo_mode=1, block_size=4096, n_samples=4096 * 5, write_total=0,
+                             predictor=3, order=8, plant_sync_every=2, seed=93).flac
     cases = {  # name: (stream, streams the planner finishes of the 3 in the batch)
-        "min_frame_ok": (st.flac, 0),
+        "plain": (st.flac, 0),
         "trailing_3_bytes": (st.flac + b"\x00\x01\x02", 0),
-        "min_frame_too_large": (_with_min_frame(st.flac, avail // 2), 3),
-        "min_frame_unknown": (_with_min_frame(st.flac, 0), 3),
+        "min_frame_too_large": (_with_min_frame(st.flac, avail // 2), 0),
+        "min_frame_unknown": (_with_min_frame(st.flac, 0), 0),
         "trailing_4_bytes": (st.flac + b"\x00\x01\x02\x03", 3),
+        "planted_syncs": (planted, 3),
     }
     for name, (data, seq) in cases.items():
         r = oracle.decode(data)
@@ -427,6 +430,24 @@ def test_unknown_total_certified_by_parallel_pass(gpu_ready):
         b.close()
     assert oracle.decode(st.flac).error == "OK"
     assert oracle.decode(st.flac + b"\x00\x01\x02\x03").error != "OK"
+
+
+def test_unknown_total_all_formats(gpu_ready):
+    """Every parity config written with STREAMINFO total 0, in one batch: samples equal to the
+    oracle's, and every stream certified by the parallel pass (k_verify to EOF; the formats,
+    channel counts, block sizes and the variable-blocking stream all reserved by the
+    creation's pre-scan), none left to the sequential planner."""
+    names = sorted(PARITY_CONFIGS)
+    sts = [synth.generate(**dict(PARITY_CONFIGS[n], write_total=0, seed=4600 + i)) for i, n in enumerate(names)]
+    b = zflac_amd.Batch([st.flac for st in sts], timing=True)
+    b.run()
+    assert b.timings().sequential_streams == 0
+    for i, (n, st) in enumerate(zip(names, sts)):
+        r = oracle.decode(st.flac)
+        assert b.error_name(i) == r.error, n
+        if r.error == "OK":
+            np.testing.assert_array_equal(b.read(i).samples.values, r.samples, err_msg=n)
+    b.close()
 
 
 def test_pipelined_device_md5_overlapped(gpu_ready):

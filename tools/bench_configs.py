@@ -52,7 +52,7 @@ ROWS = {
     "6-channel 24-bit LPC-10": (dict(channels=6, bps=24, order=10, precision=14, block_size=B, noise_lsb=64.0), 128,
                                 SAT, False),
     "C3, 2600 frames (a ~4-minute track)": (synth.config_c3(), 2600, 2600, False),
-    "C3, total unknown (sequential planner)": (synth.config_c3(), 256, 4096, True),
+    "C3, total unknown (parallel pass since round 6)": (synth.config_c3(), 256, 4096, True),
     "C3, planted false syncs (repair path)": (dict(channels=2, bps=16, stereo_mode=1, order=8, block_size=B,
                                                    plant_sync_every=2), 256, 4096, False),
     # every header's CRC-8 byte wrong (zflac ignores it): the indexer drops every header and

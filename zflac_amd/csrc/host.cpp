@@ -133,7 +133,6 @@ struct ByteReader {
 
 struct StreamInfoH {
     uint16_t min_block = 0, max_block = 0;
-    uint32_t min_frame = 0;  // bytes (0: unknown)
     uint32_t sample_rate = 0;
     uint32_t channels = 0;  // count
     uint32_t bps = 0;       // bits
@@ -159,7 +158,6 @@ int parse_metadata(const uint8_t* d, size_t n, StreamInfoH& si, size_t& frames_b
             const uint8_t* p = d + r.pos;
             si.min_block = (uint16_t)((p[0] << 8) | p[1]);
             si.max_block = (uint16_t)((p[2] << 8) | p[3]);
-            si.min_frame = ((uint32_t)p[4] << 16) | ((uint32_t)p[5] << 8) | p[6];
             si.sample_rate = ((uint32_t)p[10] << 12) | ((uint32_t)p[11] << 4) | (p[12] >> 4);
             si.channels = ((p[12] >> 1) & 7) + 1;
             si.bps = (((p[12] & 1) << 4) | (p[13] >> 4)) + 1;
@@ -570,19 +568,44 @@ uint32_t plan_buckets(const zflac_batch* b, const Class& C, const zflac_stream* 
 }
 
 // Output room for a stream whose STREAMINFO total is 0 (unknown): zflac then reads frames until
-// fewer than 4 bytes are left (src/zflac.zig:343-350) and grows its buffer as it goes. The fast
-// path reserves room for every frame the stream can hold by STREAMINFO's minimum frame size and
-// maximum block size; a chain that does not fit it (STREAMINFO wrong) is not certified
-// (k_verify) and goes to the sequential planner, as does a stream without a minimum frame
-// size. 0 = no reservation.
-uint64_t unknown_total_cap(const StreamState& s) {
-    if (!s.si.min_frame) return 0;
-    const uint64_t avail = s.len - s.frames_begin;
-    const uint64_t frames = avail / s.si.min_frame + 1;
-    const uint64_t cap = frames * (s.si.max_block ? s.si.max_block : 65535u) * (uint64_t)s.nch;
-    // (a memory bound: at most 32 output elements per input byte, ~2x the least compressed
-    // 16-bit stereo stream (verbatim) would need)
-    return cap <= 32 * avail + (1u << 20) ? cap : 0;
+// fewer than 4 bytes are left (src/zflac.zig:343-350) and grows its buffer as it goes. Once per
+// batch (here, at creation) a k_scan over the class gives every stream's frame-sync candidates
+// and the sample units their headers claim; the chain zflac walks is made of candidates, so
+// their units bound its output. That is the stream's reservation, and the parallel pass then
+// certifies its chain to the end of the stream (k_verify). A stream whose candidates claim more
+// than UNKNOWN_MAX_PER_BYTE output elements per input byte (a flood of false syncs) gets no
+// reservation and goes to the sequential planner. (Silence as constant subframes, the most
+// compressible content, is ~800 elements per byte at 4,096-sample blocks.)
+constexpr uint64_t UNKNOWN_MAX_PER_BYTE = 4096;
+
+void prescan_unknown_totals(zflac_batch* b, Class& C, std::vector<uint64_t>& units, std::vector<uint64_t>& cands) {
+    hipStream_t st = b->stream;
+    ScanArgs sa;
+    sa.in = C.in.p;
+    sa.streams = C.d_desc.p;
+    sa.chunks = C.d_chunks.p;
+    sa.n_chunks = (uint32_t)C.chunks.size();
+    sa.chunk_cnt = C.chunk_cnt.p;
+    sa.chunk_units = C.chunk_units.p;
+    sa.chunk_slots = C.chunk_slots.p;
+    sa.chunk_slot_units = C.chunk_slot_units.p;
+    sa.status = C.status;
+    sa.n_status = (uint32_t)C.members.size();
+    sa.misc = C.misc.p;
+    ck(launch_scan(sa, st));
+    std::vector<uint32_t> cnt(C.chunks.size());
+    std::vector<unsigned long long> u(C.chunks.size());
+    if (!C.chunks.empty()) {
+        ck(hipMemcpyAsync(cnt.data(), C.chunk_cnt.p, cnt.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        ck(hipMemcpyAsync(u.data(), C.chunk_units.p, u.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    }
+    ck(hipStreamSynchronize(st));
+    units.assign(C.members.size(), 0);
+    cands.assign(C.members.size(), 0);
+    for (size_t k = 0; k < C.chunks.size(); k++) {
+        units[C.chunks[k].stream] += u[k];
+        cands[C.chunks[k].stream] += cnt[k];
+    }
 }
 
 void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
@@ -597,10 +620,10 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     }
     C.in_bytes = off;
     C.in.alloc(off + INPUT_PAD);
-    uint64_t out = 0;
     uint64_t est_frames = 0, grid_frames = 0;
     C.desc.resize(C.members.size());
     C.chunks.clear();
+    C.any_unknown = false;
     for (size_t m = 0; m < C.members.size(); m++) {
         StreamState& s = b->streams[C.members[m]];
         s.slot = (uint32_t)m;
@@ -608,17 +631,10 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
         std::memset(&D, 0, sizeof(D));
         D.in_begin = in_off[m] + s.frames_begin;
         D.in_end = in_off[m] + s.len;
-        // each stream's region starts on a 32-byte boundary, whatever the length of the
-        // streams before it: the packed 16-byte stores of the fast path need 16-byte aligned
-        // frames, and zflac's backing is 32-byte aligned (:331)
-        const uint64_t align_elems = 32 / (uint64_t)esz;
-        out = (out + align_elems - 1) & ~(align_elems - 1);
-        D.out_base = out;
         D.valid_total = s.si.total > 0;
         D.total = D.valid_total ? s.si.total * (uint64_t)s.nch : 0;
-        D.out_cap = D.valid_total ? D.total : unknown_total_cap(s);
-        if (!D.valid_total && D.out_cap) C.any_unknown = true;
-        out += D.out_cap;
+        D.out_cap = D.total;  // (total unknown: from the pre-scan below)
+        if (!D.valid_total) C.any_unknown = true;
         D.rate_hz = s.first.rate;
         D.si_rate = s.si.sample_rate;
         D.byte1 = (uint8_t)s.first.byte1;
@@ -639,16 +655,12 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
         D.end_chunk = (uint32_t)C.chunks.size();
         const uint64_t minb = std::max<uint64_t>(16, s.si.min_block ? s.si.min_block : 16);
         // (at most one candidate per two bytes: a huge STREAMINFO total cannot inflate it)
-        const uint64_t est =
-            std::min<uint64_t>(s.si.total ? s.si.total / minb : (s.si.min_frame ? s.len / s.si.min_frame : s.len / 16),
-                               s.len / 2) + 2;
-        est_frames += est;
+        const uint64_t est = std::min<uint64_t>(s.si.total ? s.si.total / minb : s.len / 16, s.len / 2) + 2;
+        if (D.valid_total) est_frames += est;  // (total unknown: the pre-scan's candidate count)
         // fixed blocking with a known total: zflac reads exactly ceil(total / block) frames (:341)
         const bool fixed = s.si.min_block == s.si.max_block && s.si.min_block >= 16;
-        grid_frames += (s.si.total && fixed) ? (s.si.total + s.si.min_block - 1) / s.si.min_block : est;
+        if (D.valid_total) grid_frames += fixed ? (s.si.total + s.si.min_block - 1) / s.si.min_block : est;
     }
-    C.out_elems = out;
-    C.out.alloc(out * esz + 32);
     std::vector<const uint8_t*> srcs(C.members.size());
     std::vector<uint64_t> lens(C.members.size());
     for (size_t m = 0; m < C.members.size(); m++) {
@@ -657,7 +669,6 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     }
     upload_streams(b->device, C.in.p, C.in.n, in_off, srcs, lens, b->stream);  // inputs resident in HBM
     C.d_desc.alloc(C.desc.size());
-    ck(hipMemcpy(C.d_desc.p, C.desc.data(), C.desc.size() * sizeof(StreamDesc), hipMemcpyHostToDevice));
     const size_t nc = std::max<size_t>(C.chunks.size(), 1);
     C.d_chunks.alloc(nc);
     if (!C.chunks.empty())
@@ -671,6 +682,32 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     C.misc.alloc(4 + C.members.size());
     C.status = C.misc.p + 4;
     C.dummy.alloc(DUMMY_BYTES + PROBE_BYTES);
+    if (C.any_unknown) {  // reservations of the streams without a STREAMINFO total
+        ck(hipMemcpy(C.d_desc.p, C.desc.data(), C.desc.size() * sizeof(StreamDesc), hipMemcpyHostToDevice));
+        std::vector<uint64_t> units, cands;
+        prescan_unknown_totals(b, C, units, cands);
+        for (size_t m = 0; m < C.members.size(); m++) {
+            StreamDesc& D = C.desc[m];
+            if (D.valid_total) continue;
+            const uint64_t avail = D.in_end - D.in_begin;
+            D.out_cap = units[m] <= UNKNOWN_MAX_PER_BYTE * avail + (1u << 20) ? units[m] : 0;
+            est_frames += cands[m] + 2;
+            grid_frames += cands[m] + 2;
+        }
+    }
+    // output layout: each stream's region starts on a 32-byte boundary, whatever the length of
+    // the streams before it: the packed 16-byte stores of the fast path need 16-byte aligned
+    // frames, and zflac's backing is 32-byte aligned (:331)
+    uint64_t out = 0;
+    const uint64_t align_elems = 32 / (uint64_t)esz;
+    for (StreamDesc& D : C.desc) {
+        out = (out + align_elems - 1) & ~(align_elems - 1);
+        D.out_base = out;
+        out += D.out_cap;
+    }
+    C.out_elems = out;
+    C.out.alloc(out * esz + 32);
+    ck(hipMemcpy(C.d_desc.p, C.desc.data(), C.desc.size() * sizeof(StreamDesc), hipMemcpyHostToDevice));
     const size_t units_at = (4 + C.members.size() + 1) & ~(size_t)1;  // (u32 index, 8-byte aligned)
     const size_t pin_words = units_at + (C.any_unknown ? 2 * C.members.size() : 0);
     ck(hipHostMalloc(reinterpret_cast<void**>(&C.pin.p), pin_words * sizeof(uint32_t), hipHostMallocDefault));
