@@ -89,8 +89,9 @@ def test_crc16_clean_streams_decode_unchanged(name):
 @pytest.mark.parametrize("name", ["ms16", "unknown_total", "ch6_16", "tiny_blocks"])
 @pytest.mark.parametrize("which", [0, 2, -1])
 def test_crc16_bad_trailer(name, which):
-    """A flipped trailer bit: zflac (and the default path) decode it; the check reports it,
-    on the certified path and on the sequential planner (unknown total)."""
+    """A flipped trailer bit: zflac (and the default path) decode it; the check reports it on
+    the certified path, a stream whose STREAMINFO total is unknown included (certified by the
+    parallel pass since round 6; the planner's case is test_crc16_before_later_frame_error)."""
     st = synth.generate(**CONFIGS[name])
     fr = _frames(st)
     a, e = fr[which]
