@@ -450,6 +450,38 @@ def test_unknown_total_all_formats(gpu_ready):
     b.close()
 
 
+def test_unknown_total_truncations_and_tails(gpu_ready):
+    """Total-unknown streams cut at random byte offsets (mid-frame, at frame boundaries, 1-3
+    bytes past one) or followed by random tails (garbage, a copy of a frame header, a whole
+    frame): one batch, every stream's error name and samples equal to the oracle's, whichever
+    of the parallel pass and the planner finished it."""
+    rng = np.random.default_rng(4700)
+    st = synth.generate(**dict(PARITY_CONFIGS["c3_ms16_lpc8"], write_total=0, seed=4701))
+    fo = [int(x) for x in st.frame_offsets] + [len(st.flac)]
+    datas = []
+    for _ in range(12):  # anywhere in the frame section
+        datas.append(st.flac[: int(rng.integers(st.frames_begin + 1, len(st.flac)))])
+    for b in fo[1:]:  # at a frame boundary, and 1..3 bytes past it
+        datas += [st.flac[:b], st.flac[: b + int(rng.integers(1, 4))]]
+    for n in (1, 2, 3, 4, 5, 17, 300):
+        datas.append(st.flac + rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+    datas.append(st.flac + st.flac[fo[0]: fo[0] + 8])  # a frame header with nothing after it
+    datas.append(st.flac + st.flac[fo[1]: fo[2]])  # one more whole frame
+    b = zflac_amd.Batch(datas)
+    b.run()
+    for i, data in enumerate(datas):
+        r = oracle.decode(data)
+        try:
+            d = b.read(i)
+            err = "OK"
+        except errors.ZflacError as e:
+            err, d = type(e).__name__, None
+        assert err == r.error, (i, len(data))
+        if d is not None:
+            np.testing.assert_array_equal(d.samples.values, r.samples)
+    b.close()
+
+
 def test_pipelined_device_md5_overlapped(gpu_ready):
     """ZFLAC_FLAG_DEVICE_MD5 with three batches in flight (submit / wait): the certified
     streams' digests come from the k_md5 enqueued by submit, the sequential ones (a false
