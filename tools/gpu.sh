@@ -10,8 +10,8 @@
 #                                             workload: serial (one run in flight, the isolated
 #                                             launches the roofline uses) and the bench's default
 #                                             runs in flight (four; round-4 profiles: three)
-#   tools/gpu.sh md5leg  <tag> <name> [args]  the decode+MD5 leg alone (MD5Q hardware queues, default 7 =
-#                                             bench's 5 run + 2 md5 hub streams)
+#   tools/gpu.sh md5leg  <tag> <name> [args]  the decode+MD5 leg alone (MD5Q hardware queues, default 8 =
+#                                             bench's 5 run + 3 md5 hub streams)
 #   tools/gpu.sh md5trace <tag>               rocprofv3 kernel trace of the decode+MD5 leg alone
 #   tools/gpu.sh pmc     <tag>                PMC passes (one rocprofv3 run per pass, counters only)
 #                                             + FETCH/WRITE calibration + summary (pmc_summary.json,
@@ -59,11 +59,11 @@ case $CMD in
     ;;
   md5leg)  # md5leg <tag> <name> [bench args]: the decode+MD5 leg alone
     NAME=$1; shift
-    GPU_MAX_HW_QUEUES=${MD5Q:-7} timeout -k 10 300 python bench.py --md5-only --md5-steps 48 --warmup 12 "$@" \
+    GPU_MAX_HW_QUEUES=${MD5Q:-8} timeout -k 10 300 python bench.py --md5-only --md5-steps 48 --warmup 12 "$@" \
         > $O/$NAME.json 2> $O/$NAME.err
     ;;
   md5trace)
-    export GPU_MAX_HW_QUEUES=${MD5Q:-7}  # as the bench's decode+MD5 child runs (set before rocprofv3, not via env)
+    export GPU_MAX_HW_QUEUES=${MD5Q:-8}  # as the bench's decode+MD5 child runs (set before rocprofv3, not via env)
     prof $O/md5leg python3 $R/bench.py --md5-only --md5-steps 36 --warmup 12 "$@" > $O/md5leg.log 2>&1
     ;;
   pmc)
