@@ -698,15 +698,48 @@ void alloc_class(zflac_batch* b, Class& C, const zflac_stream* src) {
     // output layout: each stream's region starts on a 32-byte boundary, whatever the length of
     // the streams before it: the packed 16-byte stores of the fast path need 16-byte aligned
     // frames, and zflac's backing is 32-byte aligned (:331)
-    uint64_t out = 0;
     const uint64_t align_elems = 32 / (uint64_t)esz;
-    for (StreamDesc& D : C.desc) {
-        out = (out + align_elems - 1) & ~(align_elems - 1);
-        D.out_base = out;
-        out += D.out_cap;
+    auto layout = [&]() {
+        uint64_t o = 0;
+        for (StreamDesc& D : C.desc) {
+            o = (o + align_elems - 1) & ~(align_elems - 1);
+            D.out_base = o;
+            o += D.out_cap;
+        }
+        return o;
+    };
+    uint64_t out = layout();
+    if (C.any_unknown) {
+        // The reservations of unknown totals come from candidate headers, which planted false
+        // syncs can inflate: together with the rest of the class they get at most half of the
+        // device's free memory (the largest dropped first, to the planner), and none at all if
+        // the allocation still fails.
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+        while (out * esz > free_b / 2) {
+            StreamDesc* big = nullptr;
+            for (StreamDesc& D : C.desc)
+                if (!D.valid_total && D.out_cap && (!big || D.out_cap > big->out_cap)) big = &D;
+            if (!big) break;
+            big->out_cap = 0;
+            out = layout();
+        }
+    }
+    try {
+        C.out.alloc(out * esz + 32);
+    } catch (const DeviceError&) {
+        bool dropped = false;
+        for (StreamDesc& D : C.desc)
+            if (!D.valid_total && D.out_cap) {
+                D.out_cap = 0;
+                dropped = true;
+            }
+        if (!dropped) throw;
+        (void)hipGetLastError();  // (the failed hipMalloc's error must not surface at a later check)
+        out = layout();
+        C.out.alloc(out * esz + 32);
     }
     C.out_elems = out;
-    C.out.alloc(out * esz + 32);
     ck(hipMemcpy(C.d_desc.p, C.desc.data(), C.desc.size() * sizeof(StreamDesc), hipMemcpyHostToDevice));
     const size_t units_at = (4 + C.members.size() + 1) & ~(size_t)1;  // (u32 index, 8-byte aligned)
     const size_t pin_words = units_at + (C.any_unknown ? 2 * C.members.size() : 0);
